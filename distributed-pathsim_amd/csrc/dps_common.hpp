@@ -1,0 +1,149 @@
+// Shared helpers for libdpathsim (gfx950 / CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstddef>
+#include <cstdint>
+
+#include "dpathsim.h"
+
+namespace dps {
+
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
+constexpr int kWave = 64;
+
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// Bump allocator over the caller's workspace (never allocates device memory).
+struct Carve {
+  char* base;
+  size_t cap;
+  size_t off = 0;
+  bool ok = true;
+  Carve(void* p, size_t n) : base(static_cast<char*>(p)), cap(n) {}
+  template <class T>
+  T* take(size_t count) {
+    size_t bytes = align_up(count * sizeof(T));
+    if (off + bytes > cap) { ok = false; return nullptr; }
+    T* p = reinterpret_cast<T*>(base + off);
+    off += bytes;
+    return p;
+  }
+};
+
+inline int grid_for(int64_t n, int block, int64_t cap = 2048 * 4) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return static_cast<int>(g);
+}
+
+// ---- wave64 primitives ------------------------------------------------------
+__device__ __forceinline__ int lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+// number of set bits of `mask` strictly below this lane
+__device__ __forceinline__ int mbcnt(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(mask), 0u));
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ unsigned readlane(unsigned v, int l) {
+  return static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(v), l));
+}
+__device__ __forceinline__ int64_t readlane(int64_t v, int l) {
+  int lo = __builtin_amdgcn_readlane(static_cast<int>(static_cast<uint64_t>(v)), l);
+  int hi = __builtin_amdgcn_readlane(static_cast<int>(static_cast<uint64_t>(v) >> 32), l);
+  return static_cast<int64_t>((static_cast<uint64_t>(static_cast<unsigned>(hi)) << 32) |
+                              static_cast<unsigned>(lo));
+}
+__device__ __forceinline__ double readlane(double v, int l) {
+  return __longlong_as_double(readlane(static_cast<int64_t>(__double_as_longlong(v)), l));
+}
+
+template <class T>
+__device__ __forceinline__ T wave_inclusive_sum(T v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    T t = __shfl_up(v, d, kWave);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+template <class T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
+  return v;
+}
+template <class T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    T o = __shfl_xor(v, d, kWave);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// Ascending bitonic sort of one int per lane across the wave.
+__device__ __forceinline__ int wave_bitonic_sort(int v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int k = 2; k <= kWave; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      int o = __shfl_xor(v, j, kWave);
+      bool up = (lane & k) == 0;
+      bool lower = (lane & j) == 0;
+      int mn = o < v ? o : v;
+      int mx = o < v ? v : o;
+      v = (lower == up) ? mn : mx;
+    }
+  }
+  return v;
+}
+
+// ---- device-wide scans (dps_scan.hip) ------------------------------------------
+// out[0..n] = exclusive prefix sums of in[0..n), out[n] = total.  ws from
+// scan_workspace_size(n).  T in {int32_t, uint32_t, int64_t}.
+size_t scan_workspace_size(int64_t n);
+template <class T>
+hipError_t scan_exclusive(const T* in, int64_t* out, int64_t n, void* ws, size_t ws_bytes,
+                          hipStream_t stream);
+
+// ---- segmented sort + unique (+ run counts) (dps_csr.hip) ----------------------
+// For every segment s: data[seg_ptr[s] .. seg_ptr[s+1]) is sorted ascending and
+// compacted in place to its distinct values (first uniq[s] slots); when
+// `counts` is non-null counts[seg_ptr[s] + i] = multiplicity of value i.
+size_t seg_unique_workspace_size(int64_t n_seg);
+hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, int64_t n_seg,
+                      int64_t* uniq, void* ws, size_t ws_bytes, hipStream_t stream);
+
+}  // namespace dps
+
+#define DPS_HIP_RET(call)                                                              \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      dps::set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #call,                \
+                     hipGetErrorString(e_));                                           \
+      return DPS_ERR_HIP;                                                              \
+    }                                                                                  \
+  } while (0)
+
+#define DPS_REQUIRE(cond, code, ...)                                                   \
+  do {                                                                                 \
+    if (!(cond)) {                                                                     \
+      dps::set_error(__VA_ARGS__);                                                     \
+      return (code);                                                                   \
+    }                                                                                  \
+  } while (0)
+
+#define DPS_LAUNCHED() DPS_HIP_RET(hipGetLastError())

@@ -1,0 +1,616 @@
+// Typed incidence extraction, typed CSR build (sort + unique = the motif's
+// distinct), expand-sort-compress SpGEMM C = W_AP . W_PX, and the global-walk
+// vectors s, g.  SURVEY.md §8a rows A2-A4.
+#include "dps_common.hpp"
+
+namespace dps {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kSegLdsCap = 12288;  // ints staged in LDS by the long-segment path (48 KiB)
+
+__device__ __forceinline__ int64_t bound_from(const int64_t* dev, int64_t host) {
+  return dev ? *dev : host;
+}
+
+// ---------------------------------------------------------------------------
+// A2: typed incidence extraction (DPathSim_APVPA.py:78-84).  Wave-aggregated
+// atomic append: one atomic per wave per output list.
+__global__ __launch_bounds__(kBlock) void k_extract(
+    const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+    const uint8_t* __restrict__ rel, int64_t n, const uint8_t* __restrict__ ntype,
+    const int32_t* __restrict__ rowid, const int32_t* __restrict__ colid,
+    int32_t* __restrict__ ap_r, int32_t* __restrict__ ap_c, unsigned long long* n_ap,
+    int32_t* __restrict__ px_r, int32_t* __restrict__ px_c, unsigned long long* n_px) {
+  const int lane = lane_id();
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  const int64_t n_round = (n + kWave - 1) / kWave * kWave;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n_round;
+       i += stride) {
+    bool is_ap = false, is_px = false;
+    int32_t s = 0, d = 0;
+    if (i < n) {
+      s = src[i];
+      d = dst[i];
+      const uint8_t r = rel[i];
+      const uint8_t td = ntype[d];
+      is_ap = (r == DPS_R_AP) && (td == DPS_T_PAPER);
+      is_px = (r == DPS_R_PX) && (ntype[s] == DPS_T_PAPER) && (td == DPS_T_MID);
+    }
+    const uint64_t m_ap = ballot(is_ap);
+    const uint64_t m_px = ballot(is_px);
+    unsigned long long b_ap = 0, b_px = 0;
+    if (lane == 0) {
+      if (m_ap) b_ap = atomicAdd(n_ap, static_cast<unsigned long long>(__popcll(m_ap)));
+      if (m_px) b_px = atomicAdd(n_px, static_cast<unsigned long long>(__popcll(m_px)));
+    }
+    b_ap = __shfl(b_ap, 0, kWave);
+    b_px = __shfl(b_px, 0, kWave);
+    if (is_ap) {
+      const int64_t o = static_cast<int64_t>(b_ap) + mbcnt(m_ap);
+      ap_r[o] = rowid[s];
+      ap_c[o] = colid[d];
+    }
+    if (is_px) {
+      const int64_t o = static_cast<int64_t>(b_px) + mbcnt(m_px);
+      px_r[o] = colid[s];
+      px_c[o] = colid[d];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Counting-sort scatter of (row, col) pairs into row segments.
+__global__ __launch_bounds__(kBlock) void k_count_rows(const int32_t* __restrict__ rows,
+                                                       int64_t cap, const int64_t* n_dev,
+                                                       uint32_t* __restrict__ cnt) {
+  const int64_t n = bound_from(n_dev, cap);
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kBlock)
+    atomicAdd(&cnt[rows[i]], 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_scatter_rows(
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ cols, int64_t cap,
+    const int64_t* n_dev, const int64_t* __restrict__ seg_ptr, uint32_t* __restrict__ cursor,
+    int32_t* __restrict__ tmp) {
+  const int64_t n = bound_from(n_dev, cap);
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int32_t r = rows[i];
+    tmp[seg_ptr[r] + atomicAdd(&cursor[r], 1u)] = cols[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Segmented sort + unique (+ run lengths).
+// Short segments (<= 64): one wave, bitonic sort in registers.
+__global__ __launch_bounds__(kBlock) void k_seg_short(int32_t* __restrict__ data,
+                                                      int32_t* __restrict__ counts,
+                                                      const int64_t* __restrict__ seg_ptr,
+                                                      int64_t n_seg, int64_t* __restrict__ uniq,
+                                                      int32_t* __restrict__ long_list,
+                                                      unsigned* __restrict__ n_long) {
+  const int lane = lane_id();
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  for (int64_t s = wave0; s < n_seg; s += nwaves) {
+    const int64_t beg = seg_ptr[s];
+    const int len = static_cast<int>(seg_ptr[s + 1] - beg);
+    if (len > kWave) {
+      if (lane == 0) long_list[atomicAdd(n_long, 1u)] = static_cast<int32_t>(s);
+      continue;
+    }
+    if (len == 0) {
+      if (lane == 0) uniq[s] = 0;
+      continue;
+    }
+    int v = lane < len ? data[beg + lane] : INT_MAX;
+    v = wave_bitonic_sort(v);
+    const int prev = __shfl_up(v, 1, kWave);
+    const bool first = lane < len && (lane == 0 || v != prev);
+    const uint64_t mask = ballot(first);
+    if (first) {
+      const int rank = mbcnt(mask);
+      data[beg + rank] = v;
+      if (counts) {
+        const uint64_t above = mask & ~((2ull << lane) - 1ull);
+        const int next = above ? (__ffsll(static_cast<long long>(above)) - 1) : len;
+        counts[beg + rank] = next - lane;
+      }
+    }
+    if (lane == 0) uniq[s] = __popcll(mask);
+  }
+}
+
+// Ascending bitonic network over a[0..len) with virtual +inf padding to a
+// power of two.  Every comparator puts the minimum at the lower index
+// ("flip" formulation), so padded slots never need to be materialised.
+__device__ void block_bitonic_sort(int32_t* a, int len) {
+  int n2 = 1;
+  while (n2 < len) n2 <<= 1;
+  const int half_n = n2 >> 1;
+  for (int k = 2; k <= n2; k <<= 1) {
+    const int half = k >> 1;
+    for (int p = threadIdx.x; p < half_n; p += blockDim.x) {
+      const int blk = p / half, off = p - blk * half;
+      const int i = blk * k + off, j = blk * k + k - 1 - off;
+      if (j < len) {
+        const int32_t ai = a[i], aj = a[j];
+        if (aj < ai) { a[i] = aj; a[j] = ai; }
+      }
+    }
+    __syncthreads();
+    for (int jd = half >> 1; jd > 0; jd >>= 1) {
+      for (int p = threadIdx.x; p < half_n; p += blockDim.x) {
+        const int blk = p / jd, off = p - blk * jd;
+        const int i = blk * 2 * jd + off, j = i + jd;
+        if (j < len) {
+          const int32_t ai = a[i], aj = a[j];
+          if (aj < ai) { a[i] = aj; a[j] = ai; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ int64_t block_excl_scan_int(int v, int64_t* lds_w, int64_t* total) {
+  const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
+  int64_t inc = wave_inclusive_sum(static_cast<int64_t>(v));
+  if (lane == kWave - 1) lds_w[wave] = inc;
+  __syncthreads();
+  int64_t off = 0, tot = 0;
+  for (int w = 0; w < kWavesPerBlock; ++w) {
+    if (w < wave) off += lds_w[w];
+    tot += lds_w[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return off + inc - v;
+}
+
+// Long segments: one block each; staged in LDS when they fit, else sorted in
+// place in global memory.  Then unique (+ run lengths) in 256-element chunks.
+__global__ __launch_bounds__(kBlock) void k_seg_long(int32_t* __restrict__ data,
+                                                     int32_t* __restrict__ counts,
+                                                     const int64_t* __restrict__ seg_ptr,
+                                                     int64_t* __restrict__ uniq,
+                                                     const int32_t* __restrict__ long_list,
+                                                     const unsigned* __restrict__ n_long) {
+  extern __shared__ __attribute__((aligned(16))) int32_t lds_seg[];
+  __shared__ int64_t lds_w[kWavesPerBlock];
+  __shared__ int32_t lds_prev;
+  const unsigned nl = *n_long;
+  for (unsigned li = blockIdx.x; li < nl; li += gridDim.x) {
+    const int64_t s = long_list[li];
+    const int64_t beg = seg_ptr[s];
+    const int len = static_cast<int>(seg_ptr[s + 1] - beg);
+    int32_t* a;
+    if (len <= kSegLdsCap) {
+      for (int i = threadIdx.x; i < len; i += kBlock) lds_seg[i] = data[beg + i];
+      __syncthreads();
+      a = lds_seg;
+    } else {
+      a = data + beg;
+    }
+    block_bitonic_sort(a, len);
+    int64_t carry = 0;
+    for (int c0 = 0; c0 < len; c0 += kBlock) {
+      const int i = c0 + threadIdx.x;
+      const bool valid = i < len;
+      const int32_t v = valid ? a[i] : 0;
+      int32_t prev = 0;
+      if (valid && i > 0) prev = (threadIdx.x == 0) ? lds_prev : a[i - 1];
+      const bool first = valid && (i == 0 || v != prev);
+      __syncthreads();  // every read of this chunk happens before any write below
+      if (threadIdx.x == kBlock - 1 || i == len - 1) lds_prev = v;
+      int64_t tot;
+      const int64_t rank = carry + block_excl_scan_int(first ? 1 : 0, lds_w, &tot);
+      if (first) {
+        data[beg + rank] = v;
+        if (counts) counts[beg + rank] = i;  // position for now; turned into lengths below
+      }
+      carry += tot;
+      __syncthreads();
+    }
+    if (counts) {
+      for (int64_t u0 = 0; u0 < carry; u0 += kBlock) {
+        const int64_t u = u0 + threadIdx.x;
+        int32_t here = 0, next = 0;
+        if (u < carry) {
+          here = counts[beg + u];
+          next = (u + 1 < carry) ? counts[beg + u + 1] : len;
+        }
+        __syncthreads();
+        if (u < carry) counts[beg + u] = next - here;
+        __syncthreads();
+      }
+    }
+    if (threadIdx.x == 0) uniq[s] = carry;
+    __syncthreads();
+  }
+}
+
+// Compact segment heads into the final CSR arrays.
+__global__ __launch_bounds__(kBlock) void k_compact(const int32_t* __restrict__ tmp,
+                                                    const int32_t* __restrict__ tmp_cnt,
+                                                    const int64_t* __restrict__ seg_ptr,
+                                                    const int64_t* __restrict__ out_ptr,
+                                                    int64_t n_seg, int32_t* __restrict__ col,
+                                                    int32_t* __restrict__ val) {
+  const int lane = lane_id();
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  for (int64_t s = wave0; s < n_seg; s += nwaves) {
+    const int64_t src = seg_ptr[s];
+    const int64_t dst = out_ptr[s];
+    const int64_t len = out_ptr[s + 1] - dst;
+    for (int64_t i = lane; i < len; i += kWave) {
+      col[dst + i] = tmp[src + i];
+      if (val) val[dst + i] = tmp_cnt[src + i];
+    }
+  }
+}
+
+__global__ void k_copy_scalar(const int64_t* src, int64_t* dst) { *dst = *src; }
+
+// ---------------------------------------------------------------------------
+// SpGEMM (expand-sort-compress).  Wave per output row.
+__device__ __forceinline__ int64_t out_row_src(const int32_t* rows, int64_t i) {
+  return rows ? static_cast<int64_t>(rows[i]) : i;
+}
+
+__global__ __launch_bounds__(kBlock) void k_expand_len(const int64_t* __restrict__ ap_ptr,
+                                                       const int32_t* __restrict__ ap_col,
+                                                       const int32_t* __restrict__ rows,
+                                                       int64_t n_out,
+                                                       const int64_t* __restrict__ px_ptr,
+                                                       int64_t* __restrict__ e_len,
+                                                       unsigned long long* e_total) {
+  const int lane = lane_id();
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  for (int64_t i = wave0; i < n_out; i += nwaves) {
+    const int64_t r = out_row_src(rows, i);
+    const int64_t b = ap_ptr[r], e = ap_ptr[r + 1];
+    int64_t sum = 0;
+    for (int64_t j = b + lane; j < e; j += kWave) {
+      const int32_t p = ap_col[j];
+      sum += px_ptr[p + 1] - px_ptr[p];
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) {
+      if (e_len) e_len[i] = sum;
+      if (e_total) atomicAdd(e_total, static_cast<unsigned long long>(sum));
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_expand(const int64_t* __restrict__ ap_ptr,
+                                                   const int32_t* __restrict__ ap_col,
+                                                   const int32_t* __restrict__ rows, int64_t n_out,
+                                                   const int64_t* __restrict__ px_ptr,
+                                                   const int32_t* __restrict__ px_col,
+                                                   const int64_t* __restrict__ exp_ptr,
+                                                   int32_t* __restrict__ tmp) {
+  const int lane = lane_id();
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  for (int64_t i = wave0; i < n_out; i += nwaves) {
+    const int64_t r = out_row_src(rows, i);
+    const int64_t b = ap_ptr[r], e = ap_ptr[r + 1];
+    int64_t out = exp_ptr[i];
+    for (int64_t c0 = b; c0 < e; c0 += kWave) {
+      const int64_t j = c0 + lane;
+      int64_t pb = 0, pl = 0;
+      if (j < e) {
+        const int32_t p = ap_col[j];
+        pb = px_ptr[p];
+        pl = px_ptr[p + 1] - pb;
+      }
+      const int64_t inc = wave_inclusive_sum(pl);
+      int64_t o = out + inc - pl;
+      for (int64_t t = 0; t < pl; ++t) tmp[o + t] = px_col[pb + t];
+      out += readlane(inc, kWave - 1);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// A4: s[v] = sum_{(p,v) in PX} indeg_AP(p);  g = C.s, diag, stats.
+__global__ __launch_bounds__(kBlock) void k_paper_indeg(const int64_t* __restrict__ ap_ptr,
+                                                        const int32_t* __restrict__ ap_col,
+                                                        int64_t n_rows,
+                                                        int32_t* __restrict__ indeg) {
+  const int64_t nnz = ap_ptr[n_rows];
+  for (int64_t j = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; j < nnz;
+       j += static_cast<int64_t>(gridDim.x) * kBlock)
+    atomicAdd(&indeg[ap_col[j]], 1);
+}
+
+__global__ __launch_bounds__(kBlock) void k_mid_walks(const int64_t* __restrict__ px_ptr,
+                                                      const int32_t* __restrict__ px_col,
+                                                      int64_t n_papers,
+                                                      const int32_t* __restrict__ indeg,
+                                                      unsigned long long* __restrict__ s) {
+  for (int64_t p = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; p < n_papers;
+       p += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int d = indeg[p];
+    if (d == 0) continue;
+    for (int64_t j = px_ptr[p]; j < px_ptr[p + 1]; ++j)
+      atomicAdd(&s[px_col[j]], static_cast<unsigned long long>(d));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_global_walks(const int64_t* __restrict__ c_ptr,
+                                                         const int32_t* __restrict__ c_col,
+                                                         const int32_t* __restrict__ c_val,
+                                                         int64_t n_rows,
+                                                         const int64_t* __restrict__ s,
+                                                         int64_t* __restrict__ g,
+                                                         int64_t* __restrict__ diag,
+                                                         unsigned long long* __restrict__ stats) {
+  const int lane = lane_id();
+  int64_t max_c = 0, max_d = 0, max_g = 0;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  const int64_t n_round = (n_rows + kWave - 1) / kWave * kWave;
+  for (int64_t x = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; x < n_round;
+       x += stride) {
+    if (x < n_rows) {
+      int64_t gx = 0, dx = 0;
+      for (int64_t j = c_ptr[x]; j < c_ptr[x + 1]; ++j) {
+        const int64_t c = c_val[j];
+        gx += c * s[c_col[j]];
+        dx += c * c;
+        max_c = c > max_c ? c : max_c;
+      }
+      g[x] = gx;
+      if (diag) diag[x] = dx;
+      max_d = dx > max_d ? dx : max_d;
+      max_g = gx > max_g ? gx : max_g;
+    }
+  }
+  max_c = wave_max(max_c);
+  max_d = wave_max(max_d);
+  max_g = wave_max(max_g);
+  if (lane == 0 && stats) {
+    atomicMax(&stats[DPS_STAT_MAX_C], static_cast<unsigned long long>(max_c));
+    atomicMax(&stats[DPS_STAT_MAX_DIAG], static_cast<unsigned long long>(max_d));
+    atomicMax(&stats[DPS_STAT_MAX_G], static_cast<unsigned long long>(max_g));
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && stats)
+    stats[DPS_STAT_NNZ_C] = static_cast<unsigned long long>(c_ptr[n_rows] - c_ptr[0]);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+size_t seg_unique_workspace_size(int64_t n_seg) {
+  return align_up(static_cast<size_t>(n_seg > 0 ? n_seg : 1) * sizeof(int32_t)) + 256;
+}
+
+hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, int64_t n_seg,
+                      int64_t* uniq, void* ws, size_t ws_bytes, hipStream_t stream) {
+  Carve c(ws, ws_bytes);
+  int32_t* long_list = c.take<int32_t>(n_seg > 0 ? n_seg : 1);
+  unsigned* n_long = c.take<unsigned>(1);
+  if (!c.ok) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(n_long, 0, sizeof(unsigned), stream);
+  if (e != hipSuccess) return e;
+  if (n_seg <= 0) return hipSuccess;
+  k_seg_short<<<grid_for(n_seg * kWave, kBlock), kBlock, 0, stream>>>(data, counts, seg_ptr,
+                                                                      n_seg, uniq, long_list,
+                                                                      n_long);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  k_seg_long<<<512, kBlock, kSegLdsCap * sizeof(int32_t), stream>>>(data, counts, seg_ptr, uniq,
+                                                                   long_list, n_long);
+  return hipGetLastError();
+}
+
+}  // namespace dps
+
+using namespace dps;
+
+extern "C" {
+
+int dps_extract_incidence(const int32_t* edge_src, const int32_t* edge_dst,
+                          const uint8_t* edge_rel, int64_t n_edges, const uint8_t* node_type,
+                          const int32_t* node_rowid, const int32_t* node_colid, int64_t n_nodes,
+                          int32_t* ap_row, int32_t* ap_col, int64_t* n_ap, int32_t* px_row,
+                          int32_t* px_col, int64_t* n_px, void* stream) {
+  DPS_REQUIRE(n_edges >= 0 && n_nodes >= 0, DPS_ERR_INVALID, "negative size");
+  DPS_REQUIRE(n_ap && n_px, DPS_ERR_INVALID, "null count output");
+  auto st = static_cast<hipStream_t>(stream);
+  DPS_HIP_RET(hipMemsetAsync(n_ap, 0, sizeof(int64_t), st));
+  DPS_HIP_RET(hipMemsetAsync(n_px, 0, sizeof(int64_t), st));
+  if (n_edges == 0) return DPS_OK;
+  DPS_REQUIRE(edge_src && edge_dst && edge_rel && node_type && node_rowid && node_colid &&
+                  ap_row && ap_col && px_row && px_col,
+              DPS_ERR_INVALID, "null array");
+  k_extract<<<grid_for(n_edges, kBlock), kBlock, 0, st>>>(
+      edge_src, edge_dst, edge_rel, n_edges, node_type, node_rowid, node_colid, ap_row, ap_col,
+      reinterpret_cast<unsigned long long*>(n_ap), px_row, px_col,
+      reinterpret_cast<unsigned long long*>(n_px));
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+size_t dps_csr_build_workspace_size(int64_t n_pairs, int64_t n_rows) {
+  const size_t nr = static_cast<size_t>(n_rows > 0 ? n_rows : 1);
+  const size_t np = static_cast<size_t>(n_pairs > 0 ? n_pairs : 1);
+  size_t s = 0;
+  s += align_up(nr * sizeof(uint32_t));           // cnt
+  s += align_up(nr * sizeof(uint32_t));           // cursor
+  s += align_up((nr + 1) * sizeof(int64_t));      // seg_ptr
+  s += align_up(nr * sizeof(int64_t));            // uniq
+  s += align_up(np * sizeof(int32_t));            // tmp
+  s += align_up(scan_workspace_size(n_rows + 1));
+  s += align_up(seg_unique_workspace_size(n_rows));
+  return s + 1024;
+}
+
+int dps_csr_build(const int32_t* rows, const int32_t* cols, int64_t n_pairs,
+                  const int64_t* n_pairs_dev, int64_t n_rows, int64_t* row_ptr, int32_t* col_out,
+                  int64_t* nnz_out, void* ws, size_t ws_bytes, void* stream) {
+  DPS_REQUIRE(n_pairs >= 0 && n_rows >= 0, DPS_ERR_INVALID, "negative size");
+  DPS_REQUIRE(n_rows < INT32_MAX, DPS_ERR_OVERFLOW, "n_rows %lld exceeds int32",
+              static_cast<long long>(n_rows));
+  DPS_REQUIRE(row_ptr && nnz_out, DPS_ERR_INVALID, "null output");
+  DPS_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 256 == 0, DPS_ERR_WORKSPACE,
+              "workspace not 256-byte aligned");
+  DPS_REQUIRE(ws_bytes >= dps_csr_build_workspace_size(n_pairs, n_rows), DPS_ERR_WORKSPACE,
+              "csr_build workspace too small: %zu < %zu", ws_bytes,
+              dps_csr_build_workspace_size(n_pairs, n_rows));
+  auto st = static_cast<hipStream_t>(stream);
+  Carve c(ws, ws_bytes);
+  const int64_t nr = n_rows > 0 ? n_rows : 1;
+  uint32_t* cnt = c.take<uint32_t>(nr);
+  uint32_t* cursor = c.take<uint32_t>(nr);
+  int64_t* seg_ptr = c.take<int64_t>(nr + 1);
+  int64_t* uniq = c.take<int64_t>(nr);
+  int32_t* tmp = c.take<int32_t>(n_pairs > 0 ? n_pairs : 1);
+  const size_t scan_ws = scan_workspace_size(n_rows + 1);
+  void* sws = c.take<char>(scan_ws);
+  const size_t seg_ws = seg_unique_workspace_size(n_rows);
+  void* gws = c.take<char>(seg_ws);
+  DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "csr_build workspace carve failed");
+
+  DPS_HIP_RET(hipMemsetAsync(cnt, 0, nr * sizeof(uint32_t), st));
+  DPS_HIP_RET(hipMemsetAsync(cursor, 0, nr * sizeof(uint32_t), st));
+  if (n_pairs > 0) {
+    DPS_REQUIRE(rows && cols, DPS_ERR_INVALID, "null input pairs");
+    k_count_rows<<<grid_for(n_pairs, kBlock), kBlock, 0, st>>>(rows, n_pairs, n_pairs_dev, cnt);
+    DPS_LAUNCHED();
+  }
+  DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, seg_ptr, n_rows, sws, scan_ws, st));
+  if (n_pairs > 0) {
+    k_scatter_rows<<<grid_for(n_pairs, kBlock), kBlock, 0, st>>>(rows, cols, n_pairs, n_pairs_dev,
+                                                                 seg_ptr, cursor, tmp);
+    DPS_LAUNCHED();
+  }
+  DPS_HIP_RET(seg_unique(tmp, nullptr, seg_ptr, n_rows, uniq, gws, seg_ws, st));
+  DPS_HIP_RET(scan_exclusive<int64_t>(uniq, row_ptr, n_rows, sws, scan_ws, st));
+  if (n_rows > 0) {
+    k_compact<<<grid_for(n_rows * kWave, kBlock), kBlock, 0, st>>>(tmp, nullptr, seg_ptr, row_ptr,
+                                                                   n_rows, col_out, nullptr);
+    DPS_LAUNCHED();
+  }
+  k_copy_scalar<<<1, 1, 0, st>>>(row_ptr + n_rows, nnz_out);
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+int dps_spgemm_expand_size(const int64_t* ap_ptr, const int32_t* ap_col, const int32_t* rows,
+                           int64_t n_out_rows, const int64_t* px_ptr, int64_t* e_total,
+                           void* stream) {
+  DPS_REQUIRE(n_out_rows >= 0, DPS_ERR_INVALID, "negative size");
+  DPS_REQUIRE(e_total, DPS_ERR_INVALID, "null output");
+  auto st = static_cast<hipStream_t>(stream);
+  DPS_HIP_RET(hipMemsetAsync(e_total, 0, sizeof(int64_t), st));
+  if (n_out_rows == 0) return DPS_OK;
+  k_expand_len<<<grid_for(n_out_rows * kWave, kBlock), kBlock, 0, st>>>(
+      ap_ptr, ap_col, rows, n_out_rows, px_ptr, nullptr,
+      reinterpret_cast<unsigned long long*>(e_total));
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+size_t dps_spgemm_workspace_size(int64_t n_out_rows, int64_t expand_cap) {
+  const size_t n = static_cast<size_t>(n_out_rows > 0 ? n_out_rows : 1);
+  const size_t e = static_cast<size_t>(expand_cap > 0 ? expand_cap : 1);
+  size_t s = 0;
+  s += align_up(n * sizeof(int64_t));         // e_len
+  s += align_up((n + 1) * sizeof(int64_t));   // exp_ptr
+  s += align_up(n * sizeof(int64_t));         // uniq
+  s += align_up(e * sizeof(int32_t));         // tmp
+  s += align_up(e * sizeof(int32_t));         // counts
+  s += align_up(scan_workspace_size(n_out_rows + 1));
+  s += align_up(seg_unique_workspace_size(n_out_rows));
+  return s + 1024;
+}
+
+int dps_spgemm_count(const int64_t* ap_ptr, const int32_t* ap_col, const int32_t* rows,
+                     int64_t n_out_rows, const int64_t* px_ptr, const int32_t* px_col,
+                     int64_t n_papers, int64_t* c_ptr, int32_t* c_col, int32_t* c_val,
+                     int64_t* c_nnz, int64_t expand_cap, void* ws, size_t ws_bytes,
+                     void* stream) {
+  (void)n_papers;
+  DPS_REQUIRE(n_out_rows >= 0 && expand_cap >= 0, DPS_ERR_INVALID, "negative size");
+  DPS_REQUIRE(c_ptr && c_nnz, DPS_ERR_INVALID, "null output");
+  DPS_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 256 == 0, DPS_ERR_WORKSPACE,
+              "workspace not 256-byte aligned");
+  DPS_REQUIRE(ws_bytes >= dps_spgemm_workspace_size(n_out_rows, expand_cap), DPS_ERR_WORKSPACE,
+              "spgemm workspace too small");
+  DPS_REQUIRE(!c_col == !c_val, DPS_ERR_INVALID, "c_col and c_val must both be set (numeric)");
+  auto st = static_cast<hipStream_t>(stream);
+  Carve c(ws, ws_bytes);
+  const int64_t n = n_out_rows > 0 ? n_out_rows : 1;
+  int64_t* e_len = c.take<int64_t>(n);
+  int64_t* exp_ptr = c.take<int64_t>(n + 1);
+  int64_t* uniq = c.take<int64_t>(n);
+  int32_t* tmp = c.take<int32_t>(expand_cap > 0 ? expand_cap : 1);
+  int32_t* cnt = c.take<int32_t>(expand_cap > 0 ? expand_cap : 1);
+  const size_t scan_ws = scan_workspace_size(n_out_rows + 1);
+  void* sws = c.take<char>(scan_ws);
+  const size_t seg_ws = seg_unique_workspace_size(n_out_rows);
+  void* gws = c.take<char>(seg_ws);
+  DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "spgemm workspace carve failed");
+
+  if (c_col == nullptr) {  // symbolic: expand, sort, unique+count; keep results in ws
+    if (n_out_rows > 0) {
+      k_expand_len<<<grid_for(n_out_rows * kWave, kBlock), kBlock, 0, st>>>(
+          ap_ptr, ap_col, rows, n_out_rows, px_ptr, e_len, nullptr);
+      DPS_LAUNCHED();
+    }
+    DPS_HIP_RET(scan_exclusive<int64_t>(e_len, exp_ptr, n_out_rows, sws, scan_ws, st));
+    if (n_out_rows > 0) {
+      k_expand<<<grid_for(n_out_rows * kWave, kBlock), kBlock, 0, st>>>(
+          ap_ptr, ap_col, rows, n_out_rows, px_ptr, px_col, exp_ptr, tmp);
+      DPS_LAUNCHED();
+    }
+    DPS_HIP_RET(seg_unique(tmp, cnt, exp_ptr, n_out_rows, uniq, gws, seg_ws, st));
+    DPS_HIP_RET(scan_exclusive<int64_t>(uniq, c_ptr, n_out_rows, sws, scan_ws, st));
+    k_copy_scalar<<<1, 1, 0, st>>>(c_ptr + n_out_rows, c_nnz);
+    DPS_LAUNCHED();
+    return DPS_OK;
+  }
+  if (n_out_rows > 0) {  // numeric: compact (workspace of the symbolic call, unmodified)
+    k_compact<<<grid_for(n_out_rows * kWave, kBlock), kBlock, 0, st>>>(tmp, cnt, exp_ptr, c_ptr,
+                                                                       n_out_rows, c_col, c_val);
+    DPS_LAUNCHED();
+  }
+  return DPS_OK;
+}
+
+int dps_mid_walks(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_ap_rows,
+                  const int64_t* px_ptr, const int32_t* px_col, int64_t n_papers, int64_t n_mids,
+                  int32_t* paper_indeg_ws, int64_t* s, void* stream) {
+  DPS_REQUIRE(n_ap_rows >= 0 && n_papers >= 0 && n_mids >= 0, DPS_ERR_INVALID, "negative size");
+  auto st = static_cast<hipStream_t>(stream);
+  if (n_mids > 0) DPS_HIP_RET(hipMemsetAsync(s, 0, n_mids * sizeof(int64_t), st));
+  if (n_papers == 0) return DPS_OK;
+  DPS_HIP_RET(hipMemsetAsync(paper_indeg_ws, 0, n_papers * sizeof(int32_t), st));
+  k_paper_indeg<<<2048, kBlock, 0, st>>>(ap_ptr, ap_col, n_ap_rows, paper_indeg_ws);
+  DPS_LAUNCHED();
+  k_mid_walks<<<grid_for(n_papers, kBlock), kBlock, 0, st>>>(
+      px_ptr, px_col, n_papers, paper_indeg_ws, reinterpret_cast<unsigned long long*>(s));
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+int dps_global_walks(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                     int64_t n_rows, const int64_t* s, int64_t* g, int64_t* diag, int64_t* stats,
+                     void* stream) {
+  DPS_REQUIRE(n_rows >= 0, DPS_ERR_INVALID, "negative size");
+  auto st = static_cast<hipStream_t>(stream);
+  if (stats) DPS_HIP_RET(hipMemsetAsync(stats, 0, DPS_STATS_LEN * sizeof(int64_t), st));
+  k_global_walks<<<grid_for(n_rows, kBlock), kBlock, 0, st>>>(
+      c_ptr, c_col, c_val, n_rows, s, g, diag, reinterpret_cast<unsigned long long*>(stats));
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+}  // extern "C"

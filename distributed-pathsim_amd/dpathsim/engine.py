@@ -1,0 +1,298 @@
+"""Device pipeline: typed CSR build -> SpGEMM C -> s, g -> C^T tiles -> top-k.
+
+Every stage is a libdpathsim (HIP, gfx950) call on the current PyTorch-ROCm
+stream; PyTorch only allocates device memory.  Replaces the graphframes motif
+queries of DPathSim_APVPA.py:70-109 (see include/dpathsim.h per entry point).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+from .graph import TypedTables
+
+DEFAULT_TILE_W = 4096
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+@dataclass
+class BuildInfo:
+    n_nodes: int = 0
+    n_edges: int = 0
+    n_authors: int = 0
+    n_papers: int = 0
+    n_mids: int = 0
+    nnz_ap: int = 0
+    nnz_px: int = 0
+    expand: int = 0
+    nnz_c: int = 0
+    max_c: int = 0
+    max_diag: int = 0
+    max_g: int = 0
+    phase_ms: dict = field(default_factory=dict)
+
+
+class PathSimEngine:
+    """All device state for one graph + meta-path on one GPU."""
+
+    def __init__(self, typed: TypedTables, device=None, tile_w: int = DEFAULT_TILE_W):
+        if not torch.cuda.is_available():
+            raise RuntimeError("PathSimEngine needs a ROCm GPU (torch.cuda.is_available() is False);"
+                               " there is no CPU fallback")
+        _lib.load()
+        self.typed = typed
+        self.device = torch.device(device if device is not None else "cuda")
+        if tile_w & (tile_w - 1) or not 256 <= tile_w <= 16384:
+            raise ValueError("tile_w must be a power of two in [256, 16384]")
+        self.tile_w = int(tile_w)
+        self.info = BuildInfo()
+        self.built = False
+        self._dev = {}
+
+    # ------------------------------------------------------------------ utils
+    @property
+    def stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _empty(self, n, dtype):
+        return torch.empty(max(int(n), 1), dtype=dtype, device=self.device)
+
+    def _ws(self, nbytes):
+        return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+
+    # ----------------------------------------------------------------- upload
+    def upload(self):
+        """Host -> HBM copy of the typed node tables and the raw edge list."""
+        t = self.typed
+        g = t.graph
+        with torch.cuda.device(self.device):
+            to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device, non_blocking=False)
+            self._dev.update(
+                edge_src=to(g.edge_src if g.n_edges else np.zeros(1, np.int32)),
+                edge_dst=to(g.edge_dst if g.n_edges else np.zeros(1, np.int32)),
+                edge_rel=to(t.edge_rel if g.n_edges else np.zeros(1, np.uint8)),
+                node_type=to(t.node_type if g.n_nodes else np.zeros(1, np.uint8)),
+                node_rowid=to(t.node_rowid if g.n_nodes else np.zeros(1, np.int32)),
+                node_colid=to(t.node_colid if g.n_nodes else np.zeros(1, np.int32)),
+            )
+        return self
+
+    # ------------------------------------------------------------------ build
+    def build(self, timed: bool = False):
+        """Run the device build.  Inputs must be uploaded (resident in HBM)."""
+        if "edge_src" not in self._dev:
+            self.upload()
+        t = self.typed
+        d = self._dev
+        st = self.stream
+        N, E = t.graph.n_nodes, t.graph.n_edges
+        NA, NP, NV = t.n_authors, t.n_papers, t.n_mids
+        info = self.info = BuildInfo(n_nodes=N, n_edges=E, n_authors=NA, n_papers=NP, n_mids=NV)
+        marks = []
+
+        def mark(name):
+            if timed:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                marks.append((name, ev))
+
+        with torch.cuda.device(self.device):
+            mark("start")
+            # A2: typed incidence extraction
+            ap_r, ap_c = self._empty(E, torch.int32), self._empty(E, torch.int32)
+            px_r, px_c = self._empty(E, torch.int32), self._empty(E, torch.int32)
+            n_ap = self._empty(1, torch.int64)
+            n_px = self._empty(1, torch.int64)
+            _lib.call("dps_extract_incidence", _ptr(d["edge_src"]), _ptr(d["edge_dst"]),
+                      _ptr(d["edge_rel"]), E, _ptr(d["node_type"]), _ptr(d["node_rowid"]),
+                      _ptr(d["node_colid"]), N, _ptr(ap_r), _ptr(ap_c), _ptr(n_ap),
+                      _ptr(px_r), _ptr(px_c), _ptr(n_px), st)
+            mark("extract")
+            # A2/A3: typed CSR build (distinct)
+            ws_bytes = max(_lib.size("dps_csr_build_workspace_size", E, N),
+                           _lib.size("dps_csr_build_workspace_size", E, NP))
+            ws = self._ws(ws_bytes)
+            ap_ptr, ap_col = self._empty(N + 1, torch.int64), self._empty(E, torch.int32)
+            ap_nnz = self._empty(1, torch.int64)
+            _lib.call("dps_csr_build", _ptr(ap_r), _ptr(ap_c), E, _ptr(n_ap), N, _ptr(ap_ptr),
+                      _ptr(ap_col), _ptr(ap_nnz), _ptr(ws), ws.numel(), st)
+            px_ptr, px_col = self._empty(NP + 1, torch.int64), self._empty(E, torch.int32)
+            px_nnz = self._empty(1, torch.int64)
+            _lib.call("dps_csr_build", _ptr(px_r), _ptr(px_c), E, _ptr(n_px), NP, _ptr(px_ptr),
+                      _ptr(px_col), _ptr(px_nnz), _ptr(ws), ws.numel(), st)
+            del ap_r, ap_c, px_r, px_c
+            mark("csr")
+            # A3: SpGEMM C = W_AP . W_PX over author rows [0, NA)
+            e_tot = self._empty(1, torch.int64)
+            _lib.call("dps_spgemm_expand_size", _ptr(ap_ptr), _ptr(ap_col), None, NA, _ptr(px_ptr),
+                      _ptr(e_tot), st)
+            expand = int(e_tot.item())                       # sync 1: size the workspace
+            sws = self._ws(_lib.size("dps_spgemm_workspace_size", NA, expand))
+            c_ptr, c_nnz = self._empty(NA + 1, torch.int64), self._empty(2, torch.int64)
+            _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, NA, _ptr(px_ptr),
+                      _ptr(px_col), NP, _ptr(c_ptr), None, None, _ptr(c_nnz), expand, _ptr(sws),
+                      sws.numel(), st)
+            nnz_c = int(c_nnz[0].item())                     # sync 2: allocate C
+            c_col, c_val = self._empty(nnz_c, torch.int32), self._empty(nnz_c, torch.int32)
+            _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, NA, _ptr(px_ptr),
+                      _ptr(px_col), NP, _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(c_nnz),
+                      expand, _ptr(sws), sws.numel(), st)
+            del sws
+            mark("spgemm")
+            # A4: s (over ALL AP rows), g = C.s, diag, stats
+            s = self._empty(NV, torch.int64)
+            indeg = self._empty(NP, torch.int32)
+            _lib.call("dps_mid_walks", _ptr(ap_ptr), _ptr(ap_col), N, _ptr(px_ptr), _ptr(px_col),
+                      NP, NV, _ptr(indeg), _ptr(s), st)
+            g = self._empty(NA, torch.int64)
+            diag = self._empty(NA, torch.int64)
+            stats = self._empty(_lib.STATS_LEN, torch.int64)
+            _lib.call("dps_global_walks", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NA, _ptr(s),
+                      _ptr(g), _ptr(diag), _ptr(stats), st)
+            mark("walks")
+            # A5 operand layout: target-tiled C^T
+            T = max(1, math.ceil(NA / self.tile_w)) if NA else 1
+            tile_off = self._empty(NV * T + 1, torch.int32)
+            tile_ent = self._empty(nnz_c, torch.int32)
+            status = self._empty(1, torch.int32)
+            tws = self._ws(_lib.size("dps_ct_tiles_workspace_size", NV, NA, self.tile_w))
+            if nnz_c >= 2 ** 32:
+                raise OverflowError("nnz(C) >= 2^32 exceeds the uint32 tile offsets")
+            _lib.call("dps_ct_tiles_build", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NA, NV,
+                      self.tile_w, _ptr(tile_off), _ptr(tile_ent), _ptr(status), _ptr(tws),
+                      tws.numel(), st)
+            mark("tiles")
+            host = torch.cat([stats, status.to(torch.int64), ap_nnz, px_nnz]).cpu()  # sync 3
+            del tws
+        info.expand = expand
+        info.nnz_c = nnz_c
+        info.max_c = int(host[_lib.STAT_MAX_C])
+        info.max_diag = int(host[_lib.STAT_MAX_DIAG])
+        info.max_g = int(host[_lib.STAT_MAX_G])
+        info.nnz_ap = int(host[_lib.STATS_LEN + 1])
+        info.nnz_px = int(host[_lib.STATS_LEN + 2])
+        if int(host[_lib.STATS_LEN]) != 0 or info.max_c > 0xFFFF:
+            raise OverflowError(f"max C[x,v] = {info.max_c} exceeds the 16-bit tile packing")
+        if info.max_diag >= 2 ** 31:
+            raise OverflowError(f"max M[x,x] = {info.max_diag} exceeds the int32 accumulators")
+        if info.max_g >= 2 ** 52:
+            raise OverflowError("g exceeds 2^52: gx+gy would not be exact in fp64")
+        if timed:
+            torch.cuda.synchronize(self.device)
+            for (a, ea), (b, eb) in zip(marks, marks[1:]):
+                info.phase_ms[b] = ea.elapsed_time(eb)
+        d.update(ap_ptr=ap_ptr, ap_col=ap_col, px_ptr=px_ptr, px_col=px_col, c_ptr=c_ptr,
+                 c_col=c_col, c_val=c_val, s=s, g=g, diag=diag, tile_off=tile_off,
+                 tile_ent=tile_ent, topk_ws=self._ws(_lib.size("dps_cct_topk_workspace_size")))
+        self.built = True
+        return self
+
+    # ------------------------------------------------------------- accessors
+    def tensor(self, name):
+        return self._dev[name]
+
+    @property
+    def n_targets(self):
+        return self.typed.n_authors
+
+    # ------------------------------------------------------------------ top-k
+    def topk(self, k: int, row_begin: int = 0, row_end: int | None = None, out=None):
+        """★ all-pairs top-k for author rows [row_begin, row_end) (device tensors)."""
+        if not self.built:
+            raise RuntimeError("call build() first")
+        NA = self.typed.n_authors
+        row_end = NA if row_end is None else int(row_end)
+        R = row_end - row_begin
+        d = self._dev
+        if R < 0:
+            raise ValueError("row_end < row_begin")
+        if out is None:
+            out = (torch.empty((R, k), dtype=torch.int32, device=self.device),
+                   torch.empty((R, k), dtype=torch.int64, device=self.device),
+                   torch.empty((R, k), dtype=torch.float64, device=self.device))
+        idx, cnt, sc = out
+        if R == 0:
+            return idx, cnt, sc
+        with torch.cuda.device(self.device):
+            _lib.call("dps_cct_topk", _ptr(d["c_ptr"]), _ptr(d["c_col"]), _ptr(d["c_val"]),
+                      _ptr(d["g"]), NA, self.typed.n_mids, self.tile_w, _ptr(d["tile_off"]),
+                      _ptr(d["tile_ent"]), int(row_begin), int(row_end), int(k),
+                      _ptr(idx), _ptr(cnt), _ptr(sc), _ptr(d["topk_ws"]), d["topk_ws"].numel(),
+                      self.stream)
+        return idx, cnt, sc
+
+    # -------------------------------------------------------- single source
+    def source_row(self, node_index: int):
+        """Sparse C row (cols, vals device tensors) of ANY node (DPathSim_APVPA.py:77)."""
+        d = self._dev
+        t = self.typed
+        rid = int(t.node_rowid[node_index])
+        if rid < t.n_authors:
+            b, e = (int(v) for v in d["c_ptr"][rid:rid + 2].cpu())
+            return d["c_col"][b:e], d["c_val"][b:e]
+        st = self.stream
+        with torch.cuda.device(self.device):
+            rows = torch.tensor([rid], dtype=torch.int32, device=self.device)
+            e_tot = self._empty(1, torch.int64)
+            _lib.call("dps_spgemm_expand_size", _ptr(d["ap_ptr"]), _ptr(d["ap_col"]), _ptr(rows),
+                      1, _ptr(d["px_ptr"]), _ptr(e_tot), st)
+            expand = int(e_tot.item())
+            ws = self._ws(_lib.size("dps_spgemm_workspace_size", 1, expand))
+            c_ptr, c_nnz = self._empty(2, torch.int64), self._empty(2, torch.int64)
+            _lib.call("dps_spgemm_count", _ptr(d["ap_ptr"]), _ptr(d["ap_col"]), _ptr(rows), 1,
+                      _ptr(d["px_ptr"]), _ptr(d["px_col"]), t.n_papers, _ptr(c_ptr), None, None,
+                      _ptr(c_nnz), expand, _ptr(ws), ws.numel(), st)
+            nnz = int(c_nnz[0].item())
+            col, val = self._empty(nnz, torch.int32), self._empty(nnz, torch.int32)
+            _lib.call("dps_spgemm_count", _ptr(d["ap_ptr"]), _ptr(d["ap_col"]), _ptr(rows), 1,
+                      _ptr(d["px_ptr"]), _ptr(d["px_col"]), t.n_papers, _ptr(c_ptr), _ptr(col),
+                      _ptr(val), _ptr(c_nnz), expand, _ptr(ws), ws.numel(), st)
+        return col[:nnz], val[:nnz]
+
+    def global_walk(self, node_index: int) -> int:
+        """metapath_global_walk (DPathSim_APVPA.py:70-88) for any node."""
+        col, val = self.source_row(node_index)
+        with torch.cuda.device(self.device):
+            ptr = torch.tensor([0, col.numel()], dtype=torch.int64, device=self.device)
+            g = self._empty(1, torch.int64)
+            _lib.call("dps_global_walks", _ptr(ptr), _ptr(col), _ptr(val), 1, _ptr(self._dev["s"]),
+                      _ptr(g), None, None, self.stream)
+            return int(g.item())
+
+    def walk_row(self, node_index: int):
+        """Dense pairwise walks of one source against every author (int64 device)."""
+        col, val = self.source_row(node_index)
+        d = self._dev
+        NA = self.typed.n_authors
+        out = self._empty(NA, torch.int64)
+        with torch.cuda.device(self.device):
+            _lib.call("dps_walk_row", _ptr(col), _ptr(val), col.numel(), NA, self.typed.n_mids,
+                      self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]), _ptr(out),
+                      self.stream)
+        return out[:NA]
+
+    def pairwise_walk(self, a_index: int, b_index: int) -> int:
+        """metapath_pairwise_walk (DPathSim_APVPA.py:90-109) for any two nodes."""
+        ac, av = self.source_row(a_index)
+        bc, bv = self.source_row(b_index)
+        with torch.cuda.device(self.device):
+            out = self._empty(1, torch.int64)
+            _lib.call("dps_pair_count", _ptr(ac), _ptr(av), ac.numel(), _ptr(bc), _ptr(bv),
+                      bc.numel(), _ptr(out), self.stream)
+            return int(out.item())
+
+
+def build_engine(typed: TypedTables, device=None, tile_w=DEFAULT_TILE_W, timed=False):
+    t0 = time.perf_counter()
+    eng = PathSimEngine(typed, device=device, tile_w=tile_w).upload()
+    eng.build(timed=timed)
+    eng.info.phase_ms["host_total"] = (time.perf_counter() - t0) * 1e3
+    return eng

@@ -1,0 +1,207 @@
+/*
+ * dpathsim.h -- C ABI of libdpathsim.so, the MI355X (gfx950) PathSim engine.
+ *
+ * This is the drop-in boundary for the reference's hot path.
+ * The reference (phamtheanhphu/Distributed-PathSim, DPathSim_APVPA.py) has no
+ * FFI: its "operator API" is a graphframes motif query + Spark SQL filters +
+ * distinct().count() called from the Python class DPathSim_APVPA.  Each entry
+ * point below names the reference element it replaces (file:line into
+ * /root/reference).  The Python host package (dpathsim, ctypes) mirrors the
+ * reference class on top of these; INTEGRATION.md shows the bindings.
+ *
+ * Conventions
+ *  - Every function returns int status: 0 = DPS_OK, < 0 = error code; the
+ *    message is in dps_last_error() (thread-local).  No C++ exception crosses
+ *    the ABI.
+ *  - All array pointers are DEVICE pointers (allocated by the caller, e.g. as
+ *    PyTorch-ROCm tensors) unless the parameter name ends in _host.
+ *  - Work is enqueued asynchronously on the caller's hipStream_t `stream`
+ *    (passed as void*; NULL = the legacy default stream).  Outputs are valid
+ *    after the stream is synchronised.  No function allocates device memory
+ *    or synchronises the stream, except where documented ("syncs").
+ *  - Scratch comes from a caller workspace `ws` of `ws_bytes` bytes; the
+ *    matching *_workspace_size() gives the required size.  `ws` must be
+ *    256-byte aligned.
+ *  - Not re-entrant per stream; one host thread may drive several devices
+ *    (call hipSetDevice / pass that device's stream).
+ *
+ * Index spaces (built host-side from node types only, see dpathsim/graph.py):
+ *  - node n in [0, N_nodes): GEXF node order (DPathSim_APVPA.py:120-121).
+ *  - node_rowid[n]: author-typed nodes get [0, N_A) in node order, every other
+ *    node N_A + its ordinal among non-author nodes.  Rows < N_A are the
+ *    PathSim sources/targets (DPathSim_APVPA.py:18-22).
+ *  - node_colid[n]: paper ordinal for paper-typed nodes, mid (venue) ordinal
+ *    for mid-typed nodes, -1 otherwise.
+ *  - node_type[n]: DPS_T_AUTHOR / DPS_T_PAPER / DPS_T_MID / DPS_T_OTHER.
+ *  - edge_rel[e]: DPS_R_AP (relationship 'author_of'), DPS_R_PX ('submit_at'
+ *    for APVPA), DPS_R_OTHER.
+ */
+#ifndef DPATHSIM_H
+#define DPATHSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPS_ABI_VERSION 1
+
+enum {
+  DPS_OK = 0,
+  DPS_ERR_INVALID = -1,    /* bad argument / shape */
+  DPS_ERR_HIP = -2,        /* HIP runtime error */
+  DPS_ERR_WORKSPACE = -3,  /* workspace too small or misaligned */
+  DPS_ERR_OVERFLOW = -4,   /* value does not fit the engine's integer widths */
+  DPS_ERR_UNSUPPORTED = -5 /* parameter outside the supported range (e.g. k) */
+};
+
+enum { DPS_T_OTHER = 0, DPS_T_AUTHOR = 1, DPS_T_PAPER = 2, DPS_T_MID = 3 };
+enum { DPS_R_OTHER = 0, DPS_R_AP = 1, DPS_R_PX = 2 };
+
+/* Stats slots written by dps_global_walks (int64 device array, DPS_STATS_LEN). */
+enum {
+  DPS_STAT_MAX_C = 0,     /* max C[x,v] over author rows */
+  DPS_STAT_MAX_DIAG = 1,  /* max M[x,x] = sum_v C[x,v]^2 over author rows */
+  DPS_STAT_MAX_G = 2,     /* max g[x] over author rows */
+  DPS_STAT_NNZ_C = 3,     /* nnz of C (author rows) */
+  DPS_STATS_LEN = 8
+};
+
+int dps_abi_version(void);
+const char* dps_last_error(void);
+/* Number of visible HIP devices (hipGetDeviceCount); < 0 on error. */
+int dps_device_count(void);
+
+/* ---------------------------------------------------------------------------
+ * A2. Typed incidence extraction.
+ * Replaces the motif's typed edge filters DPathSim_APVPA.py:78-84 (and
+ * :99-105) over the edge/vertex DataFrames of :160-163:
+ *   AP pair (node_rowid[src], node_colid[dst]) for every edge with
+ *       edge_rel == DPS_R_AP and node_type[dst] == DPS_T_PAPER (src type NOT
+ *       checked, as in the reference);
+ *   PX pair (node_colid[src], node_colid[dst]) for every edge with
+ *       edge_rel == DPS_R_PX, node_type[src] == PAPER, node_type[dst] == MID.
+ * Duplicates are kept here (removed by dps_csr_build = the motif's distinct,
+ * :86).  Pair order is unspecified.  ap_* / px_* need capacity n_edges.
+ * n_ap / n_px: int64 device scalars (written, not accumulated).
+ * ------------------------------------------------------------------------- */
+int dps_extract_incidence(const int32_t* edge_src, const int32_t* edge_dst,
+                          const uint8_t* edge_rel, int64_t n_edges,
+                          const uint8_t* node_type, const int32_t* node_rowid,
+                          const int32_t* node_colid, int64_t n_nodes,
+                          int32_t* ap_row, int32_t* ap_col, int64_t* n_ap,
+                          int32_t* px_row, int32_t* px_col, int64_t* n_px,
+                          void* stream);
+
+/* ---------------------------------------------------------------------------
+ * A2/A3. Typed CSR build = sort + unique (the motif's select('*').distinct(),
+ * DPathSim_APVPA.py:86,107, which makes incidences binary -- SURVEY.md K3).
+ * Input: n_pairs (row, col) pairs; n_pairs is read from the device scalar
+ * `n_pairs_dev` if non-NULL (then `n_pairs` is the capacity), else `n_pairs`.
+ * Output: row_ptr int64[n_rows+1], col_out int32[capacity n_pairs] sorted
+ * ascending within each row, no duplicates; *nnz_out (int64 device scalar).
+ * ------------------------------------------------------------------------- */
+size_t dps_csr_build_workspace_size(int64_t n_pairs, int64_t n_rows);
+int dps_csr_build(const int32_t* rows, const int32_t* cols, int64_t n_pairs,
+                  const int64_t* n_pairs_dev, int64_t n_rows,
+                  int64_t* row_ptr, int32_t* col_out, int64_t* nnz_out,
+                  void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * A3. Author-venue count matrix C = W_AP . W_PX (the join A->P->V of the motif,
+ * DPathSim_APVPA.py:72-74): C[a,v] = |{p : (a,p) in AP, (p,v) in PX}|.
+ * Expand-sort-compress SpGEMM, two phases:
+ *   symbolic (c_col == NULL): fills c_ptr int64[n_out_rows+1]; *c_nnz = nnz.
+ *   numeric  (c_col != NULL): needs c_ptr from the symbolic call; writes
+ *            c_col int32[nnz] (ascending per row) and c_val int32[nnz].
+ * Output row i is AP row `rows[i]` if `rows` != NULL, else AP row i.
+ * `expand_cap` must be >= the expanded size sum_rows sum_{p in AP[row]} |PX[p]|
+ * returned by dps_spgemm_expand_size (int64 device scalar; the host reads it
+ * to size the workspace).  The numeric call must get the same, unmodified
+ * workspace as the preceding symbolic call (it holds the sorted runs).
+ * ------------------------------------------------------------------------- */
+int dps_spgemm_expand_size(const int64_t* ap_ptr, const int32_t* ap_col, const int32_t* rows,
+                           int64_t n_out_rows, const int64_t* px_ptr, int64_t* e_total,
+                           void* stream);
+size_t dps_spgemm_workspace_size(int64_t n_out_rows, int64_t expand_cap);
+int dps_spgemm_count(const int64_t* ap_ptr, const int32_t* ap_col,
+                     const int32_t* rows, int64_t n_out_rows,
+                     const int64_t* px_ptr, const int32_t* px_col, int64_t n_papers,
+                     int64_t* c_ptr, int32_t* c_col, int32_t* c_val, int64_t* c_nnz,
+                     int64_t expand_cap, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * A4. Global walk ingredients.
+ * dps_mid_walks: s[v] = sum over ALL AP rows r of C[r,v]
+ *   = sum_{(p,v) in PX} indeg_AP(p)  (author_2 unconstrained in the global
+ *   walk motif, DPathSim_APVPA.py:70-84).  s int64[n_mids], fully written.
+ * dps_global_walks: g[x] = sum_v C[x,v] * s[v] (metapath_global_walk :70-88),
+ *   diag[x] = M[x,x]; stats int64[DPS_STATS_LEN] (see DPS_STAT_*), written.
+ * ------------------------------------------------------------------------- */
+int dps_mid_walks(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_ap_rows,
+                  const int64_t* px_ptr, const int32_t* px_col, int64_t n_papers,
+                  int64_t n_mids, int32_t* paper_indeg_ws, int64_t* s,
+                  void* stream);
+int dps_global_walks(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                     int64_t n_rows, const int64_t* s, int64_t* g, int64_t* diag,
+                     int64_t* stats, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * A5 operand layout. Target-tiled transpose of C for the C.C^T kernels.
+ * Targets y in [0, n_targets) are cut into tiles of `tile_w` (power of two,
+ * 256..16384; the hot kernel keeps acc int32[W] + bitmap + list uint16[W] of
+ * one tile in LDS per wave).  Bucket (v, t) holds the packed entries
+ *   (C[y,v] << 16) | (y - t*tile_w)   for every y of tile t with C[y,v] > 0,
+ * stored contiguously in [v][t] order: bucket (v,t) is
+ *   tile_ent[tile_off[v*T + t] .. tile_off[v*T + t + 1]),  T = ceil(n_targets/tile_w).
+ * tile_off uint32[n_mids*T + 1], tile_ent uint32[nnz(C[0:n_targets])].
+ * Requires max C <= 65535 (DPS_ERR_OVERFLOW otherwise; checked on device,
+ * reported through *status_dev if non-NULL).  Entry order inside a bucket is
+ * unspecified (results are exact integer sums, so order-independent).
+ * ------------------------------------------------------------------------- */
+size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t tile_w);
+int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                       int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                       uint32_t* tile_off, uint32_t* tile_ent, int32_t* status_dev,
+                       void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * ★ A5+A6+A7 fused: the hot kernel.  For every source row x in
+ * [row_begin, row_end): M[x,y] = C[x,:].C[y,:] over all targets y != x
+ * (metapath_pairwise_walk :90-109), score = (double)(2*M) / (double)(g[x]+g[y])
+ * (one IEEE division, :51-52; 0/0 -> 0.0), and the top-k targets by
+ * (score desc, y asc), self excluded (:18-22).  Slots beyond n_targets-1
+ * available targets: idx -1, cnt 0, score 0.0.
+ * Outputs (row-major [row_end-row_begin][k]): out_idx int32, out_cnt int64,
+ * out_score double.  1 <= k <= 256.  Requires max M[x,x] < 2^31.
+ * ------------------------------------------------------------------------- */
+size_t dps_cct_topk_workspace_size(void);
+int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                 const int64_t* g, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                 const uint32_t* tile_off, const uint32_t* tile_ent,
+                 int64_t row_begin, int64_t row_end, int32_t k,
+                 int32_t* out_idx, int64_t* out_cnt, double* out_score,
+                 void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Single-source row (the reference's run() loop, :30-50): for one sparse C row
+ * (src_col/src_val, src_len entries, device), the dense pairwise walk
+ * out_m[y] = sum_v C[src,v] * C[y,v] for all targets y (int64[n_targets]).
+ * ------------------------------------------------------------------------- */
+int dps_walk_row(const int32_t* src_col, const int32_t* src_val, int64_t src_len,
+                 int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                 const uint32_t* tile_off, const uint32_t* tile_ent,
+                 int64_t* out_m, void* stream);
+
+/* metapath_pairwise_walk(source, target) (:90-109) for two sparse C rows with
+ * ascending columns: *out = sum_v a[v]*b[v] (int64 device scalar). */
+int dps_pair_count(const int32_t* a_col, const int32_t* a_val, int64_t a_len,
+                   const int32_t* b_col, const int32_t* b_val, int64_t b_len,
+                   int64_t* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPATHSIM_H */
