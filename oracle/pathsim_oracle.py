@@ -204,3 +204,71 @@ def single_source_log_lines(graph: OracleGraph, source_id: str):
             raise KeyError(source_id)
         out.append(f"Sim score {src_label} - {graph.labels[t]}: {score}")
     return out
+
+
+# ---------------------------------------------------------------------------
+# ctypes wrapper of the C restatement (oracle/pathsim_oracle.c, liboracle.so)
+class COracle:
+    """C/OpenMP restatement over typed int arrays (same semantics as above)."""
+
+    def __init__(self, ap_row, ap_col, px_paper, px_mid, n_rows_all, n_authors, n_papers, n_mids):
+        import ctypes as C
+        import os
+        here = os.path.dirname(os.path.abspath(__file__))
+        path = os.path.join(here, "liboracle.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        lib = C.CDLL(path)
+        P, I64 = C.c_void_p, C.c_int64
+        lib.orc_create.restype = P
+        lib.orc_create.argtypes = [I64, P, P, I64, P, P, I64, I64, I64, I64]
+        lib.orc_nnz.restype = I64
+        lib.orc_nnz.argtypes = [P]
+        lib.orc_export.argtypes = [P, P, P, P, P, P]
+        lib.orc_topk.argtypes = [P, I64, I64, C.c_int, P, P, P, C.c_int]
+        lib.orc_destroy.argtypes = [P]
+        self._lib = lib
+        a = [np.ascontiguousarray(x, dtype=np.int32) for x in (ap_row, ap_col, px_paper, px_mid)]
+        self._keep = a
+        self.n_authors, self.n_mids = int(n_authors), int(n_mids)
+        self._st = lib.orc_create(len(a[0]), a[0].ctypes.data, a[1].ctypes.data, len(a[2]),
+                                  a[2].ctypes.data, a[3].ctypes.data, int(n_rows_all),
+                                  int(n_authors), int(n_papers), int(n_mids))
+
+    @classmethod
+    def from_typed(cls, typed):
+        """From dpathsim.graph.TypedTables-like arrays (node tables + edges)."""
+        g = typed.graph
+        ap = (typed.edge_rel == 1) & (typed.node_type[g.edge_dst] == 2)
+        px = ((typed.edge_rel == 2) & (typed.node_type[g.edge_src] == 2)
+              & (typed.node_type[g.edge_dst] == 3))
+        return cls(typed.node_rowid[g.edge_src[ap]], typed.node_colid[g.edge_dst[ap]],
+                   typed.node_colid[g.edge_src[px]], typed.node_colid[g.edge_dst[px]],
+                   g.n_nodes, typed.n_authors, typed.n_papers, typed.n_mids)
+
+    def export(self):
+        nnz = self._lib.orc_nnz(self._st)
+        c_ptr = np.zeros(self.n_authors + 1, np.int64)
+        c_col = np.zeros(max(nnz, 1), np.int32)
+        c_val = np.zeros(max(nnz, 1), np.int32)
+        s = np.zeros(max(self.n_mids, 1), np.int64)
+        g = np.zeros(max(self.n_authors, 1), np.int64)
+        self._lib.orc_export(self._st, c_ptr.ctypes.data, c_col.ctypes.data, c_val.ctypes.data,
+                             s.ctypes.data, g.ctypes.data)
+        return c_ptr, c_col[:nnz], c_val[:nnz], s[: self.n_mids], g[: self.n_authors]
+
+    def topk(self, k, row_begin=0, row_end=None, threads=0):
+        row_end = self.n_authors if row_end is None else row_end
+        R = row_end - row_begin
+        idx = np.zeros((R, k), np.int32)
+        cnt = np.zeros((R, k), np.int64)
+        sc = np.zeros((R, k), np.float64)
+        self._lib.orc_topk(self._st, row_begin, row_end, k, idx.ctypes.data, cnt.ctypes.data,
+                           sc.ctypes.data, int(threads))
+        return idx, cnt, sc
+
+    def __del__(self):
+        st = getattr(self, "_st", None)
+        if st:
+            self._lib.orc_destroy(st)
+            self._st = None
