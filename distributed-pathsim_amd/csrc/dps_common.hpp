@@ -126,6 +126,14 @@ size_t seg_unique_workspace_size(int64_t n_seg);
 hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, int64_t n_seg,
                       int64_t* uniq, void* ws, size_t ws_bytes, hipStream_t stream);
 
+// ---- stable LSD radix sort of (u64 key, u32 value) pairs (dps_sort.hip) ------
+// Sorts by the low key_bits bits of the keys; vals_in == nullptr means values
+// 0..n-1.  Outputs must not alias inputs.
+size_t radix_sort_workspace_size(int64_t n);
+hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, uint64_t* keys_out,
+                            uint32_t* vals_out, int64_t n, int key_bits, void* ws,
+                            size_t ws_bytes, hipStream_t stream);
+
 }  // namespace dps
 
 #define DPS_HIP_RET(call)                                                              \

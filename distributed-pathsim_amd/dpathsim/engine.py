@@ -53,6 +53,7 @@ class PathSimEngine:
         if tile_w & (tile_w - 1) or not 256 <= tile_w <= 16384:
             raise ValueError("tile_w must be a power of two in [256, 16384]")
         self.tile_w = int(tile_w)
+        self.tile_skip = True
         self.info = BuildInfo()
         self.built = False
         self._dev = {}
@@ -158,28 +159,39 @@ class PathSimEngine:
             _lib.call("dps_global_walks", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NA, _ptr(s),
                       _ptr(g), _ptr(diag), _ptr(stats), st)
             mark("walks")
-            # A5 operand layout: target-tiled C^T
+            host = torch.cat([stats, ap_nnz, px_nnz]).cpu()      # sync 3: stats for key width
+            max_g = int(host[_lib.STAT_MAX_G])
+            # A5 operand layout: targets relabeled by ascending g, then tiled C^T
+            t_perm, t_rank = self._empty(NA, torch.int32), self._empty(NA, torch.int32)
+            g_t = self._empty(NA, torch.int64)
+            ows = self._ws(_lib.size("dps_target_order_workspace_size", NA))
+            _lib.call("dps_target_order", _ptr(g), NA, max(1, max_g.bit_length()), _ptr(t_perm),
+                      _ptr(t_rank), _ptr(g_t), _ptr(ows), ows.numel(), st)
+            del ows
+            mark("order")
             T = max(1, math.ceil(NA / self.tile_w)) if NA else 1
             tile_off = self._empty(NV * T + 1, torch.int32)
-            tile_ent = self._empty(nnz_c, torch.int32)
+            tile_maxc = self._empty(NV * T + 1, torch.int32)
+            tile_gmin = self._empty(T, torch.int64)
+            tile_ent = self._empty(nnz_c + 4, torch.int32)   # +16 B: kernel reads whole 16-B chunks
             status = self._empty(1, torch.int32)
             tws = self._ws(_lib.size("dps_ct_tiles_workspace_size", NV, NA, self.tile_w))
             if nnz_c >= 2 ** 32:
                 raise OverflowError("nnz(C) >= 2^32 exceeds the uint32 tile offsets")
-            _lib.call("dps_ct_tiles_build", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NA, NV,
-                      self.tile_w, _ptr(tile_off), _ptr(tile_ent), _ptr(status), _ptr(tws),
-                      tws.numel(), st)
+            _lib.call("dps_ct_tiles_build", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(g),
+                      _ptr(t_rank), NA, NV, self.tile_w, _ptr(tile_off), _ptr(tile_ent),
+                      _ptr(tile_maxc), _ptr(tile_gmin), _ptr(status), _ptr(tws), tws.numel(), st)
             mark("tiles")
-            host = torch.cat([stats, status.to(torch.int64), ap_nnz, px_nnz]).cpu()  # sync 3
+            status_h = int(status.item())                          # sync 4
             del tws
         info.expand = expand
         info.nnz_c = nnz_c
         info.max_c = int(host[_lib.STAT_MAX_C])
         info.max_diag = int(host[_lib.STAT_MAX_DIAG])
         info.max_g = int(host[_lib.STAT_MAX_G])
-        info.nnz_ap = int(host[_lib.STATS_LEN + 1])
-        info.nnz_px = int(host[_lib.STATS_LEN + 2])
-        if int(host[_lib.STATS_LEN]) != 0 or info.max_c > 0xFFFF:
+        info.nnz_ap = int(host[_lib.STATS_LEN])
+        info.nnz_px = int(host[_lib.STATS_LEN + 1])
+        if status_h != 0 or info.max_c > 0xFFFF:
             raise OverflowError(f"max C[x,v] = {info.max_c} exceeds the 16-bit tile packing")
         if info.max_diag >= 2 ** 31:
             raise OverflowError(f"max M[x,x] = {info.max_diag} exceeds the int32 accumulators")
@@ -190,8 +202,9 @@ class PathSimEngine:
             for (a, ea), (b, eb) in zip(marks, marks[1:]):
                 info.phase_ms[b] = ea.elapsed_time(eb)
         d.update(ap_ptr=ap_ptr, ap_col=ap_col, px_ptr=px_ptr, px_col=px_col, c_ptr=c_ptr,
-                 c_col=c_col, c_val=c_val, s=s, g=g, diag=diag, tile_off=tile_off,
-                 tile_ent=tile_ent, topk_ws=self._ws(_lib.size("dps_cct_topk_workspace_size")))
+                 c_col=c_col, c_val=c_val, s=s, g=g, diag=diag, g_t=g_t, t_perm=t_perm,
+                 t_rank=t_rank, tile_off=tile_off, tile_ent=tile_ent, tile_maxc=tile_maxc,
+                 tile_gmin=tile_gmin, topk_ws=self._ws(_lib.size("dps_cct_topk_workspace_size")))
         self.built = True
         return self
 
@@ -223,8 +236,10 @@ class PathSimEngine:
             return idx, cnt, sc
         with torch.cuda.device(self.device):
             _lib.call("dps_cct_topk", _ptr(d["c_ptr"]), _ptr(d["c_col"]), _ptr(d["c_val"]),
-                      _ptr(d["g"]), NA, self.typed.n_mids, self.tile_w, _ptr(d["tile_off"]),
-                      _ptr(d["tile_ent"]), int(row_begin), int(row_end), int(k),
+                      _ptr(d["g"]), _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA,
+                      self.typed.n_mids, self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
+                      _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]),
+                      int(row_begin), int(row_end), int(k),
                       _ptr(idx), _ptr(cnt), _ptr(sc), _ptr(d["topk_ws"]), d["topk_ws"].numel(),
                       self.stream)
         return idx, cnt, sc
@@ -274,7 +289,8 @@ class PathSimEngine:
         NA = self.typed.n_authors
         out = self._empty(NA, torch.int64)
         with torch.cuda.device(self.device):
-            _lib.call("dps_walk_row", _ptr(col), _ptr(val), col.numel(), NA, self.typed.n_mids,
+            _lib.call("dps_walk_row", _ptr(col), _ptr(val), col.numel(), _ptr(d["t_perm"]), NA,
+                      self.typed.n_mids,
                       self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]), _ptr(out),
                       self.stream)
         return out[:NA]

@@ -149,38 +149,61 @@ int dps_global_walks(const int64_t* c_ptr, const int32_t* c_col, const int32_t* 
                      int64_t* stats, void* stream);
 
 /* ---------------------------------------------------------------------------
- * A5 operand layout. Target-tiled transpose of C for the C.C^T kernels.
- * Targets y in [0, n_targets) are cut into tiles of `tile_w` (power of two,
- * 256..16384; the hot kernel keeps acc int32[W] + bitmap + list uint16[W] of
- * one tile in LDS per wave).  Bucket (v, t) holds the packed entries
- *   (C[y,v] << 16) | (y - t*tile_w)   for every y of tile t with C[y,v] > 0,
+ * A5 operand layout, step 1: target relabeling (a pure layout choice; results
+ * never depend on it).  Targets are relabeled in ascending global walk g (ties
+ * by original index) with a stable LSD radix sort over the low key_bits bits
+ * of g (key_bits >= bit length of max g).  Outputs: t_perm[label] = original,
+ * t_rank[original] = label, g_t[label] = g[t_perm[label]] (all n_targets).
+ * ------------------------------------------------------------------------- */
+size_t dps_target_order_workspace_size(int64_t n_targets);
+int dps_target_order(const int64_t* g, int64_t n_targets, int32_t key_bits,
+                     int32_t* t_perm, int32_t* t_rank, int64_t* g_t,
+                     void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * A5 operand layout, step 2: target-tiled transpose of C for the C.C^T kernels.
+ * Target labels (t_rank[y], or y if t_rank == NULL) in [0, n_targets) are cut
+ * into tiles of `tile_w` (power of two, 256..16384; the hot kernel keeps
+ * acc int32[W] + bitmap + list uint16[W] of one tile in LDS per wave).
+ * Bucket (v, t) holds the packed entries
+ *   (C[y,v] << 16) | (label(y) - t*tile_w)   for every y of tile t with C[y,v] > 0,
  * stored contiguously in [v][t] order: bucket (v,t) is
  *   tile_ent[tile_off[v*T + t] .. tile_off[v*T + t + 1]),  T = ceil(n_targets/tile_w).
  * tile_off uint32[n_mids*T + 1], tile_ent uint32[nnz(C[0:n_targets])].
- * Requires max C <= 65535 (DPS_ERR_OVERFLOW otherwise; checked on device,
- * reported through *status_dev if non-NULL).  Entry order inside a bucket is
- * unspecified (results are exact integer sums, so order-independent).
+ * Optional: tile_maxc uint32[n_mids*T + 1] = max C[y,v] per bucket;
+ * tile_gmin int64[T] = min g[y] per tile (needs g).
+ * Requires max C <= 65535 (else *status_dev = DPS_ERR_OVERFLOW).  Entry order
+ * inside a bucket is unspecified (results are exact integer sums).
  * ------------------------------------------------------------------------- */
 size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t tile_w);
 int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                       const int64_t* g, const int32_t* t_rank,
                        int64_t n_targets, int64_t n_mids, int32_t tile_w,
-                       uint32_t* tile_off, uint32_t* tile_ent, int32_t* status_dev,
+                       uint32_t* tile_off, uint32_t* tile_ent, uint32_t* tile_maxc,
+                       int64_t* tile_gmin, int32_t* status_dev,
                        void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * ★ A5+A6+A7 fused: the hot kernel.  For every source row x in
- * [row_begin, row_end): M[x,y] = C[x,:].C[y,:] over all targets y != x
- * (metapath_pairwise_walk :90-109), score = (double)(2*M) / (double)(g[x]+g[y])
- * (one IEEE division, :51-52; 0/0 -> 0.0), and the top-k targets by
- * (score desc, y asc), self excluded (:18-22).  Slots beyond n_targets-1
- * available targets: idx -1, cnt 0, score 0.0.
- * Outputs (row-major [row_end-row_begin][k]): out_idx int32, out_cnt int64,
- * out_score double.  1 <= k <= 256.  Requires max M[x,x] < 2^31.
+ * [row_begin, row_end) (original author ordinals): M[x,y] = C[x,:].C[y,:] over
+ * all targets y != x (metapath_pairwise_walk :90-109), score =
+ * (double)(2*M) / (double)(g[x]+g[y]) (one IEEE division, :51-52; 0/0 -> 0.0),
+ * and the top-k targets by (score desc, original y asc), self excluded
+ * (:18-22).  Slots beyond the n_targets-1 available targets: idx -1, cnt 0,
+ * score 0.0.  g: original order; g_t/t_perm/t_rank: the relabeling of
+ * dps_target_order (all NULL = identity labels, g_t = g); tile_* from
+ * dps_ct_tiles_build with the same t_rank (tile_gmin required, tile_maxc
+ * optional -- enables skipping tiles that cannot hold a top-k candidate).
+ * Outputs (row-major [row_end-row_begin][k]): out_idx int32 (original
+ * ordinals), out_cnt int64 (M), out_score double.  1 <= k <= 256.
+ * Requires max M[x,x] < 2^31.  ws: dps_cct_topk_workspace_size() bytes.
  * ------------------------------------------------------------------------- */
 size_t dps_cct_topk_workspace_size(void);
 int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
-                 const int64_t* g, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                 const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
+                 const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                  const uint32_t* tile_off, const uint32_t* tile_ent,
+                 const uint32_t* tile_maxc, const int64_t* tile_gmin,
                  int64_t row_begin, int64_t row_end, int32_t k,
                  int32_t* out_idx, int64_t* out_cnt, double* out_score,
                  void* ws, size_t ws_bytes, void* stream);
@@ -188,12 +211,20 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
 /* ---------------------------------------------------------------------------
  * Single-source row (the reference's run() loop, :30-50): for one sparse C row
  * (src_col/src_val, src_len entries, device), the dense pairwise walk
- * out_m[y] = sum_v C[src,v] * C[y,v] for all targets y (int64[n_targets]).
+ * out_m[y] = sum_v C[src,v] * C[y,v] for all targets y, in ORIGINAL target
+ * order (int64[n_targets]); t_perm as for dps_cct_topk (NULL = identity).
  * ------------------------------------------------------------------------- */
 int dps_walk_row(const int32_t* src_col, const int32_t* src_val, int64_t src_len,
-                 int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                 const int32_t* t_perm, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                  const uint32_t* tile_off, const uint32_t* tile_ent,
                  int64_t* out_m, void* stream);
+
+/* The reference's per-target score (:51-52) for one source row on the device:
+ * score[y] = (double)(2*m[y]) / (double)(gx + g[y]) (one IEEE division);
+ * *zero_div (int64 device scalar, may be NULL) counts targets with
+ * gx + g[y] == 0, where the reference raises ZeroDivisionError (score 0.0). */
+int dps_row_scores(const int64_t* m, const int64_t* g, int64_t gx, int64_t n, double* score,
+                   int64_t* zero_div, void* stream);
 
 /* metapath_pairwise_walk(source, target) (:90-109) for two sparse C rows with
  * ascending columns: *out = sum_v a[v]*b[v] (int64 device scalar). */

@@ -1,0 +1,140 @@
+"""CPU: host logic of the product package (loader, typed tables, generator, C ABI)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from dpathsim import _lib
+from dpathsim.gexf import read_gexf, write_gexf
+from dpathsim.graph import APTPA, APVPA, Graph
+from dpathsim.synth import synth_dblp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_GEXF = "/root/reference/dblp/dblp_small.gexf"
+
+
+def test_header_symbols_exported():
+    """libdpathsim.so loads and exports every function include/dpathsim.h declares."""
+    hdr = open(os.path.join(REPO, "include", "dpathsim.h")).read()
+    declared = set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\**\s+\**(dps_[a-z_0-9]+)\(", hdr, re.M))
+    assert len(declared) >= 15
+    lib = _lib.load()
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(_lib.exported_symbols()) == declared
+    assert lib.dps_abi_version() == 1
+
+
+def test_no_cpu_fallback_when_library_missing(monkeypatch):
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libdpathsim.so")
+    with pytest.raises(_lib.DPSLibraryError):
+        _lib.load()
+
+
+def test_engine_refuses_without_gpu(dblp_small_tuples):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from dpathsim.engine import PathSimEngine
+    t = Graph.from_tuples(*dblp_small_tuples).typed()
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        PathSimEngine(t)
+
+
+def test_typed_tables_dblp_small(dblp_small_tuples):
+    v, e = dblp_small_tuples
+    g = Graph.from_tuples(v, e)
+    t = g.typed(APVPA)
+    assert (t.n_authors, t.n_papers, t.n_mids) == (770, 1001, 85)
+    authors = [x[0] for x in v if x[2] == "author"]
+    assert [g.node_id(int(i)) for i in t.author_nodes] == authors
+    assert sorted(t.node_rowid.tolist()) == list(range(g.n_nodes))
+    assert int((t.edge_rel == _lib.R_AP).sum()) == 1265
+    assert int((t.edge_rel == _lib.R_PX).sum()) == 1001
+    assert g.vertices() == v and g.edges() == e
+
+
+def test_aptpa_codes():
+    g = synth_dblp(50, 100, 20, seed=1, metapath=APTPA)
+    t = g.typed(APTPA)
+    assert t.n_mids == 20
+    assert set(np.unique(t.edge_rel).tolist()) == {_lib.R_AP, _lib.R_PX}
+
+
+@pytest.mark.skipif(not os.path.exists(REF_GEXF), reason="reference data not present")
+def test_streaming_gexf_matches_networkx(dblp_small_tuples):
+    g = read_gexf(REF_GEXF)
+    assert g.vertices() == dblp_small_tuples[0]
+    assert g.edges() == dblp_small_tuples[1]
+
+
+def _nx_tuples(path):
+    import pathsim_oracle as po
+    return po.load_gexf_networkx(path)
+
+
+def test_gexf_roundtrip_synthetic(tmp_path):
+    g = synth_dblp(200, 500, 30, seed=4)
+    p = tmp_path / "s.gexf"
+    write_gexf(g, str(p))
+    v, e = _nx_tuples(str(p))
+    h = read_gexf(str(p))
+    assert h.vertices() == v == g.vertices()
+    assert h.edges() == e
+
+
+def test_gexf_multigraph_and_label_semantics(tmp_path):
+    """Parallel edges keep the MultiDiGraph; a repeated (u,v,id) updates in place;
+    the XML label attribute overrides the 'label' attvalue; mutual adds both ways."""
+    xml = """<?xml version='1.0' encoding='utf-8'?>
+<gexf version="1.2" xmlns="http://www.gexf.net/1.2draft">
+  <graph defaultedgetype="directed" mode="static">
+    <attributes class="edge" mode="static"><attribute id="1" title="label" type="string" /></attributes>
+    <attributes class="node" mode="static"><attribute id="0" title="node_type" type="string" /></attributes>
+    <nodes>
+      <node id="p" label="P"><attvalues><attvalue for="0" value="paper" /></attvalues></node>
+      <node id="a" label="A"><attvalues><attvalue for="0" value="author" /></attvalues></node>
+      <node id="v" label="V"><attvalues><attvalue for="0" value="venue" /></attvalues></node>
+    </nodes>
+    <edges>
+      <edge id="0" source="a" target="p"><attvalues><attvalue for="1" value="author_of" /></attvalues></edge>
+      <edge id="1" source="a" target="p"><attvalues><attvalue for="1" value="author_of" /></attvalues></edge>
+      <edge id="1" source="a" target="p"><attvalues><attvalue for="1" value="cites" /></attvalues></edge>
+      <edge id="2" source="p" target="v" label="submit_at"><attvalues><attvalue for="1" value="x" /></attvalues></edge>
+      <edge id="3" source="v" target="a" type="mutual"><attvalues><attvalue for="1" value="m" /></attvalues></edge>
+    </edges>
+  </graph>
+</gexf>"""
+    p = tmp_path / "m.gexf"
+    p.write_text(xml)
+    v, e = _nx_tuples(str(p))
+    h = read_gexf(str(p))
+    assert h.vertices() == v
+    assert h.edges() == e
+
+
+def test_synth_deterministic_and_shaped():
+    a = synth_dblp(1000, 3000, 50, seed=9)
+    b = synth_dblp(1000, 3000, 50, seed=9)
+    assert np.array_equal(a.edge_src, b.edge_src) and np.array_equal(a.edge_dst, b.edge_dst)
+    t = a.typed()
+    assert (t.n_authors, t.n_papers, t.n_mids) == (1000, 3000, 50)
+    ap = t.edge_rel == _lib.R_AP
+    # every author writes at least one paper
+    assert len(np.unique(t.node_rowid[a.edge_src[ap]])) == 1000
+
+
+def test_c_abi_rejects_bad_arguments_without_gpu():
+    """Argument validation happens host-side before any HIP call."""
+    lib = _lib.load()
+    rc = lib.dps_cct_topk(None, None, None, None, None, None, None, 10, 5, 300, None, None,
+                          None, None, 0, 10, 10, None, None, None, None, 0, None)
+    assert rc == _lib.DPS_ERR_UNSUPPORTED     # tile_w 300 is not a power of two
+    assert b"tile_w" in lib.dps_last_error()
+    rc = lib.dps_cct_topk(None, None, None, None, None, None, None, 10, 5, 256, None, None,
+                          None, None, 0, 10, 0, None, None, None, None, 0, None)
+    assert rc == _lib.DPS_ERR_UNSUPPORTED     # k = 0
+    assert lib.dps_csr_build_workspace_size(100, 10) > 0
