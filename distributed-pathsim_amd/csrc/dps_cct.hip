@@ -1,0 +1,730 @@
+// ★ Hot path: fused C.C^T + fp64 PathSim score + per-source top-k
+// (replaces metapath_pairwise_walk
+// DPathSim_APVPA.py:90-109, the score :51-52 and the target loop :18-22,36).
+//
+// Operands (see DESIGN.md "Data layout in HBM"):
+//   C      CSR over author rows: int64 row_ptr, int32 col (venue), int32 val.
+//   tiles  C^T cut into target tiles of W = 2^shift labels (targets relabeled
+//          in ascending global walk g, dps_target_order).  Bucket (v,t) holds
+//          packed uint32 entries (C[y,v] << 16) | (label(y) - t*W), buckets
+//          stored [v][t], each padded with zero entries to 16 bytes.
+//   g_t    g in label order (ascending), tile_maxc max C per bucket.
+//
+// One 256-thread workgroup (4 waves) owns one source row x at a time
+// (persistent grid, rows dequeued from an atomic counter).  For every target
+// tile t in ascending g:
+//   bound     UB = sum_v C[x,v] * maxc[v,t].  The workgroup shares tau, the
+//             best k-th score any of its waves holds; mneed = the smallest M
+//             whose score against the tile's smallest g reaches tau.  UB <
+//             mneed: no target of the tile can enter the top-k, skip it.
+//   scatter   the row's buckets (v,t) are flattened into 16-byte chunks spread
+//             over all 256 lanes; acc[y] += C[x,v]*C[y,v] with no-return
+//             ds_add_u32 into PACKED u16 accumulators (two targets per dword).
+//             UB <= 65535 proves no u16 lane can carry into its neighbour;
+//             tiles with a larger bound run "wide": two sub-passes over half
+//             the targets each, one int32 per target.
+//   epilogue  each wave scans a quarter of the accumulator (ds_read_b128),
+//             zeroes it in the same pass and keeps targets whose M reaches the
+//             threshold of their 1/64-tile segment (mseg: the same bound, with
+//             the segment's smallest g -- targets are g-sorted, so this is
+//             nearly exact and needs no global load).  Survivors are scored
+//             exactly: double(2M) / double(gx + gy), one IEEE division, into
+//             the wave's register top-k (lane i holds rank i).
+// At the row end wave 0 merges the four wave lists, then writes the ranked
+// entries, the zero-score fill (reference target order) and empty slots.
+#include "dps_common.hpp"
+
+#include <cstdlib>
+
+namespace dps {
+namespace {
+
+constexpr int kTB = 256;            // threads per workgroup
+constexpr int kNW = kTB / kWave;    // waves per workgroup
+constexpr int kU = 4;               // 16-B chunk loads in flight per lane
+constexpr int kSegs = kWave;        // threshold segments per tile (one per lane)
+constexpr int kQ = 2 * kWave;       // per-wave candidate queue (label, M) capacity
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+// ---- top-k order: score desc, then ORIGINAL target index asc ---------------
+__device__ __forceinline__ bool better(double s1, int y1, double s2, int y2) {
+  return s1 > s2 || (s1 == s2 && y1 < y2);
+}
+
+// Integer threshold: the smallest m >= 0 with fl(2m / den) >= kth.  Every
+// target y with g[y] >= g0 has gx + g[y] >= den := gx + g0, so (rounding is
+// monotone) fl(2M/(gx+g[y])) <= fl(2M/den), and m -> fl(2m/den) is
+// nondecreasing: a target with M < mneed scores strictly below kth and cannot
+// enter the top-k, ties included.  Starts one below ceil(kth*den/2), so it
+// usually settles after two divisions.
+__device__ __forceinline__ int compute_mneed(double kth, int64_t den) {
+  if (kth <= 0.0 || den <= 0) return 0;
+  const double dd = static_cast<double>(den);
+  const double r = kth * dd * 0.5;
+  if (r >= 2147483000.0) return INT32_MAX;
+  double m = ceil(r) - 1.0;               // integers below 2^31: 2m is exact
+  if (m < 0.0) m = 0.0;
+  if ((2.0 * m) / dd >= kth) {
+#pragma clang loop vectorize(disable) unroll(disable)
+    while (m > 0.0 && (2.0 * (m - 1.0)) / dd >= kth) m -= 1.0;
+  } else {
+    m += 1.0;
+#pragma clang loop vectorize(disable) unroll(disable)
+    while ((2.0 * m) / dd < kth) m += 1.0;
+  }
+  return static_cast<int>(m);
+}
+
+// Register-resident sorted top-k of one wave: rank r*64 + lane in slot r.
+template <int KPL>
+struct TopK {
+  double s[KPL];
+  int y[KPL];
+  int m[KPL];
+  int k;
+  int filled;
+  double kth_s;
+  int kth_y;
+
+  __device__ void init(int k_) {
+#pragma unroll
+    for (int r = 0; r < KPL; ++r) { s[r] = -1.0; y[r] = INT_MAX; m[r] = 0; }
+    k = k_;
+    filled = 0;
+    kth_s = -1.0;
+    kth_y = INT_MAX;
+  }
+  __device__ bool full() const { return filled == k; }
+  // Insert a candidate known to beat the k-th entry (wave-uniform arguments).
+  __device__ void insert(double cs, int cy, int cm) {
+    const int lane = lane_id();
+    int pos = 0;
+#pragma unroll
+    for (int r = 0; r < KPL; ++r) {
+      const bool b = (r * kWave + lane < k) && better(s[r], y[r], cs, cy);
+      pos += __popcll(ballot(b));
+    }
+    double us[KPL];
+    int uy[KPL], um[KPL];
+#pragma unroll
+    for (int r = 0; r < KPL; ++r) {
+      us[r] = __shfl_up(s[r], 1, kWave);
+      uy[r] = __shfl_up(y[r], 1, kWave);
+      um[r] = __shfl_up(m[r], 1, kWave);
+      if (r > 0 && lane == 0) {
+        us[r] = readlane(s[r - 1], kWave - 1);
+        uy[r] = readlane(y[r - 1], kWave - 1);
+        um[r] = readlane(m[r - 1], kWave - 1);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < KPL; ++r) {
+      const int slot = r * kWave + lane;
+      if (slot > pos) { s[r] = us[r]; y[r] = uy[r]; m[r] = um[r]; }
+      else if (slot == pos) { s[r] = cs; y[r] = cy; m[r] = cm; }
+    }
+    filled = filled < k ? filled + 1 : k;
+    const int rk = (k - 1) / kWave, lk = (k - 1) % kWave;
+#pragma unroll
+    for (int r = 0; r < KPL; ++r)
+      if (r == rk) { kth_s = readlane(s[r], lk); kth_y = readlane(y[r], lk); }
+  }
+};
+
+struct CctParams {
+  const int64_t* c_ptr;
+  const int32_t* c_col;
+  const int32_t* c_val;
+  const int64_t* g;          // original order (sources)
+  const int64_t* g_t;        // label order (targets, ascending)
+  const int32_t* t_perm;     // label -> original (nullable = identity)
+  const int32_t* t_rank;     // original -> label (nullable = identity)
+  const uint32_t* tile_off;
+  const uint32_t* tile_ent;
+  const uint32_t* tile_maxc; // tile_off stands in when no bounds are given
+  bool use_bounds;           // false: no skipping, every tile wide
+  const int64_t* tile_gmin;
+  int64_t n_targets;
+  int64_t T;
+  int shift;
+  int64_t row_begin;
+  int64_t n_rows;
+  int k;
+  int32_t* out_idx;
+  int64_t* out_cnt;
+  double* out_score;
+  unsigned long long* counter;
+  int ablate;                // profiling aid (DPATHSIM_ABLATE): 1 no LDS adds, 2 no
+                             // candidate scoring, 4 no scatter
+};
+
+// Up to 64 venues of the row for one tile (lane j = venue g0 + j).
+struct Grp {
+  uint32_t base; // lane j: lo_j - 4*pre_j, so chunk q of venue j is at base_j + 4q
+  int c;         // C[x, v_j]
+  int pre;       // exclusive prefix of chunk counts
+  int nq;        // total chunks (wave-uniform)
+  int nv;        // venues in the group (wave-uniform, <= 64)
+};
+
+__device__ __forceinline__ void grp_set(Grp& G, uint32_t lo, uint32_t hi, int c, int nv) {
+  G.c = c;
+  const int nch = static_cast<int>((hi - lo) >> 2);
+  const int inc = wave_inclusive_sum(nch);
+  G.pre = inc - nch;
+  G.base = lo - 4u * static_cast<uint32_t>(G.pre);
+  G.nq = readlane(inc, kWave - 1);
+  G.nv = nv;
+}
+
+constexpr int kSmallGroup = 8;
+
+// Venue owning chunk q = the largest j < nv with pre_j <= q.  Small groups:
+// compare against the prefix held in SGPRs (sp[]); larger ones: binary search
+// over ceil(log2(nv)) shuffle steps.  All lanes must run it.
+__device__ __forceinline__ int chunk_venue(const Grp& G, const int (&sp)[kSmallGroup], int q) {
+  if (G.nv <= kSmallGroup) {
+    int j = 0;
+#pragma unroll
+    for (int jj = 1; jj < kSmallGroup; ++jj) j += (jj < G.nv && q >= sp[jj]) ? 1 : 0;
+    return j;
+  }
+  int step = 1;
+  while (step * 2 < G.nv) step *= 2;
+  int j = 0;
+  for (; step > 0; step >>= 1) {
+    const int cand = j + step;
+    const int pv = __shfl(G.pre, cand & (kWave - 1), kWave);
+    if (cand < G.nv && pv <= q) j = cand;
+  }
+  return j;
+}
+
+// One accumulation pass over one target tile.  A tile whose bound UB fits in
+// 8 bits accumulates four targets per dword in one pass (99.8 % of the tiles
+// scanned on config3); UB <= 65535 takes two passes over half the tile at 16
+// bits, larger bounds four passes at 32 bits.  UB bounds every accumulator of
+// the tile, so no lane can carry into its neighbour.
+struct Stage {
+  Grp G;
+  int64_t t;
+  int lnp;       // log2(number of passes): 0 u8, 1 u16, 2 u32
+  int pass;
+  int nb;        // batches of kTB*kU chunks (0 under the no-scatter ablation)
+  int64_t gq;    // lane s: smallest g of segment s of tile t
+};
+
+struct Batch {
+  uint4 e[kU];
+  int c[kU];
+};
+
+// Issue the loads of batch b of stage S: chunk q -> lane (q mod 256) of the
+// workgroup, kU chunks per lane.
+__device__ __forceinline__ void issue(const Stage& S, int b, const uint32_t* __restrict__ ent,
+                                      int wave, int lane, Batch& B, bool no_add) {
+  int sp[kSmallGroup];
+#pragma unroll
+  for (int jj = 0; jj < kSmallGroup; ++jj) sp[jj] = readlane(S.G.pre, jj);
+  const int q0 = b * (kTB * kU) + wave * kWave + lane;
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int q = q0 + u * kTB;
+    const int j = chunk_venue(S.G, sp, q);
+    const uint32_t bj = static_cast<uint32_t>(__shfl(static_cast<int>(S.G.base), j, kWave));
+    const int cj = __shfl(S.G.c, j, kWave);
+    const bool live = q < S.G.nq;
+    B.e[u] = *reinterpret_cast<const uint4*>(ent + (live ? bj + 4u * static_cast<uint32_t>(q) : 0u));
+    B.c[u] = live && !no_add ? cj : 0;
+  }
+}
+
+__device__ __forceinline__ void acc_add(uint32_t* acc, uint32_t e, int c, int lnp, int pass,
+                                        int shift) {
+  const uint32_t yl = e & 0xFFFFu;
+  const uint32_t val = static_cast<uint32_t>(c) * (e >> 16);
+  if (val == 0) return;
+  uint32_t* dst;
+  uint32_t add;
+  if (lnp == 0) {
+    dst = acc + (yl >> 2);
+    add = val << ((yl & 3u) << 3);
+  } else {
+    if (static_cast<int>(yl >> (shift - lnp)) != pass) return;
+    const uint32_t local = yl & ((1u << (shift - lnp)) - 1u);
+    if (lnp == 1) {
+      dst = acc + (local >> 1);
+      add = val << ((local & 1u) << 4);
+    } else {
+      dst = acc + local;
+      add = val;
+    }
+  }
+  __hip_atomic_fetch_add(dst, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void scatter(const Batch& B, const Stage& S, uint32_t* acc, int shift) {
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    if (B.c[u] == 0) continue;
+    acc_add(acc, B.e[u].x, B.c[u], S.lnp, S.pass, shift);
+    acc_add(acc, B.e[u].y, B.c[u], S.lnp, S.pass, shift);
+    acc_add(acc, B.e[u].z, B.c[u], S.lnp, S.pass, shift);
+    acc_add(acc, B.e[u].w, B.c[u], S.lnp, S.pass, shift);
+  }
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Per-wave candidate queue in LDS: targets that passed the integer threshold
+// wait here so their exact scores (two global loads each) are computed 64 at
+// a time -- one memory round trip per batch instead of per find.
+struct CandQ {
+  int* lab;   // [kQ] label
+  int* m;     // [kQ] M
+  int n;      // wave-uniform fill
+};
+
+// Exact score of the first n (<= 64) queued candidates; insert those that beat
+// the wave's k-th entry and the shared tau; drop them from the queue.
+template <int KPL>
+__device__ __forceinline__ void flush(const CctParams& p, CandQ& Q, TopK<KPL>& top, int n,
+                                      int64_t gx, double tau_sh, int lane) {
+  wave_lds_fence();
+  bool cand = lane < n;
+  int M = 0, yo = 0;
+  double sc = 0.0;
+  if (cand) {
+    const int64_t label = Q.lab[lane];
+    M = Q.m[lane];
+    yo = p.t_perm ? p.t_perm[label] : static_cast<int>(label);
+    const int64_t den = gx + p.g_t[label];
+    sc = static_cast<double>(2 * static_cast<int64_t>(M)) / static_cast<double>(den);
+    cand = sc >= tau_sh && better(sc, yo, top.kth_s, top.kth_y);
+  }
+  int tl = 0, tm = 0;                      // keep the unprocessed tail at the front
+  const bool mv = lane + n < Q.n;
+  if (mv) { tl = Q.lab[lane + n]; tm = Q.m[lane + n]; }
+  wave_lds_fence();
+  if (mv) { Q.lab[lane] = tl; Q.m[lane] = tm; }
+  Q.n -= n;
+  uint64_t mask = ballot(cand);
+  if ((p.ablate & 8) && lane == 0) {       // counters: flushes, candidates, passers
+    atomicAdd(p.counter + 1, 1ull);
+    atomicAdd(p.counter + 2, static_cast<unsigned long long>(n));
+    atomicAdd(p.counter + 3, static_cast<unsigned long long>(__popcll(mask)));
+  }
+  while (mask) {
+    const int srcl = __ffsll(static_cast<long long>(mask)) - 1;
+    mask &= mask - 1;
+    const double cs = readlane(sc, srcl);
+    const int cy = readlane(yo, srcl);
+    if (!better(cs, cy, top.kth_s, top.kth_y)) continue;
+    top.insert(cs, cy, readlane(M, srcl));
+  }
+}
+
+// True if some accumulator of the 16-byte block may reach m (exact for 16 and
+// 32 bits; for 8 bits exact when m <= 128, else any byte >= 128).
+__device__ __forceinline__ bool block_any(uint4 a, uint32_t m, int lnp) {
+  if (lnp == 0) {
+    if (m > 128u) return ((a.x | a.y | a.z | a.w) & 0x80808080u) != 0;
+    const uint32_t k = (128u - m) * 0x01010101u;
+    const uint32_t f = (a.x | ((a.x & 0x7F7F7F7Fu) + k)) | (a.y | ((a.y & 0x7F7F7F7Fu) + k)) |
+                       (a.z | ((a.z & 0x7F7F7F7Fu) + k)) | (a.w | ((a.w & 0x7F7F7F7Fu) + k));
+    return (f & 0x80808080u) != 0;
+  }
+  if (lnp == 1) {
+    const us2 mx = __builtin_elementwise_max(
+        __builtin_elementwise_max(__builtin_bit_cast(us2, a.x), __builtin_bit_cast(us2, a.y)),
+        __builtin_elementwise_max(__builtin_bit_cast(us2, a.z), __builtin_bit_cast(us2, a.w)));
+    return (mx.x > mx.y ? mx.x : mx.y) >= m;
+  }
+  return max(max(a.x, a.y), max(a.z, a.w)) >= m;
+}
+
+// Scan + zero this wave's quarter of the stage's accumulator; queue the
+// targets whose M reaches their segment's threshold.
+template <int KPL>
+__device__ __forceinline__ void epilogue(const CctParams& p, uint32_t* acc, TopK<KPL>& top,
+                                         CandQ& Q, const Stage& S, int wave, int lane, int nbuf,
+                                         int seg_shift, int64_t x_lab, int64_t gx,
+                                         double tau_sh) {
+  double tau_w = tau_sh;
+  if (top.full() && top.kth_s > tau_w) tau_w = top.kth_s;
+  int mseg = 1;
+  if (tau_w > 0.0) {
+    const int mn = compute_mneed(tau_w, gx + S.gq);
+    mseg = mn > 1 ? mn : 1;
+  }
+  const int qd = nbuf / kNW;
+  const int end = (wave + 1) * qd;
+  const int lnp = S.lnp;
+  const int tpd_shift = 2 - lnp;                     // log2(targets per dword)
+  const int bits = 8 << lnp;
+  const uint32_t vmask = lnp == 2 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
+  const int64_t tile_base = S.t << p.shift;
+  const int pass_base = S.pass << (p.shift - lnp);
+  const bool score = (p.ablate & 2) == 0;
+  for (int b0 = wave * qd; b0 < end; b0 += kWave * 4) {
+    const int b = b0 + lane * 4;
+    uint4 a = make_uint4(0, 0, 0, 0);
+    if (b < end) {
+      a = *reinterpret_cast<const uint4*>(acc + b);
+      *reinterpret_cast<uint4*>(acc + b) = make_uint4(0, 0, 0, 0);
+    }
+    const int i0 = pass_base + (b << tpd_shift);            // first target of the block
+    const int ms = __shfl(mseg, (i0 >> seg_shift) & (kSegs - 1), kWave);
+    const uint32_t m = static_cast<uint32_t>(ms);
+    const bool any = block_any(a, m, lnp);
+    if (!score || !ballot(any)) continue;
+    wave_lds_fence();
+#pragma unroll 1
+    for (int v = 0; v < (16 >> lnp); ++v) {
+      const int di = v >> tpd_shift;
+      const uint32_t wv = di == 0 ? a.x : di == 1 ? a.y : di == 2 ? a.z : a.w;
+      const uint32_t M = (wv >> ((v & ((1 << tpd_shift) - 1)) * bits)) & vmask;
+      const int64_t label = tile_base + i0 + v;
+      const bool cand = any && M >= m && label != x_lab;
+      const uint64_t mk = ballot(cand);
+      if (!mk) continue;
+      if (cand) {
+        const int pos = Q.n + mbcnt(mk);
+        Q.lab[pos] = static_cast<int>(label);
+        Q.m[pos] = static_cast<int>(M);
+      }
+      Q.n += __popcll(mk);
+      if (Q.n >= kWave) flush<KPL>(p, Q, top, kWave, gx, tau_sh, lane);
+    }
+  }
+}
+
+// Bounds of the row's venues for tiles tw and tw+1 (lane j = venue j, d <= 64).
+struct Window {
+  int64_t tw;
+  int v, c;
+  uint32_t lo, hi, mx, hi1, mx1;
+};
+
+// Advance to the next tile that may hold a top-k target (d <= 64 rows).
+__device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d, int lane,
+                                           int64_t gx, double tau_sh, int seg_shift,
+                                           bool no_scatter, Stage& S) {
+  while (w.tw < p.T) {
+    const int64_t t = w.tw++;
+    const uint32_t lo = w.lo, hi = w.hi, mx = w.mx;
+    w.lo = w.hi;
+    w.hi = w.hi1;
+    w.mx = w.mx1;
+    if (lane < d && t + 2 < p.T) {
+      const int64_t vb = static_cast<int64_t>(w.v) * p.T + t + 2;
+      w.hi1 = p.tile_off[vb + 1];
+      w.mx1 = p.tile_maxc[vb];
+    }
+    int64_t ub = wave_sum(static_cast<int64_t>(w.c) * mx);
+    if (!p.use_bounds) ub = int64_t(1) << 40;
+    const bool take = ub > 0 && (tau_sh <= 0.0 || ub >= compute_mneed(tau_sh, gx + p.tile_gmin[t]));
+    if ((p.ablate & 8) && threadIdx.x == 0) {   // counters: tiles visited, tiles scanned
+      atomicAdd(p.counter + 4, 1ull);
+      if (take) atomicAdd(p.counter + 5, 1ull);
+    }
+    if (!take) continue;
+    S.t = t;
+    S.lnp = ub <= 0xFF ? 0 : ub <= 0xFFFF ? 1 : 2;
+    S.pass = 0;
+    grp_set(S.G, lo, hi, w.c, d);
+    S.nb = no_scatter ? 0 : (S.G.nq + kTB * kU - 1) / (kTB * kU);
+    S.gq = p.g_t[min((t << p.shift) + (static_cast<int64_t>(lane) << seg_shift),
+                     p.n_targets - 1)];
+    return true;
+  }
+  return false;
+}
+
+template <int KPL>
+__global__ __launch_bounds__(kTB) void k_cct_topk(CctParams p, int acc_dw) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ double tau_s[2][kNW];
+  __shared__ int fill_s[kNW];
+  __shared__ long long row_s;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = tid / kWave;
+  const int nbuf = 1 << (p.shift - 2);        // accumulator dwords per stage buffer
+  const int seg_shift = p.shift - 6;          // W / kSegs targets per threshold segment
+  const bool no_add = (p.ablate & 1) != 0;
+  const bool no_scatter = (p.ablate & 4) != 0;
+  CandQ Q;
+  Q.lab = reinterpret_cast<int*>(lds + acc_dw) + wave * 2 * kQ;
+  Q.m = Q.lab + kQ;
+  Q.n = 0;
+  for (int i = tid; i < acc_dw; i += kTB) lds[i] = 0;
+
+  for (;;) {
+    if (tid == 0) row_s = static_cast<long long>(atomicAdd(p.counter, 1ull));
+    __syncthreads();
+    const int64_t r = row_s;
+    if (r >= p.n_rows) break;
+    const int64_t x = p.row_begin + r;
+    const int64_t x_lab = p.t_rank ? static_cast<int64_t>(p.t_rank[x]) : x;
+    const int64_t pb = p.c_ptr[x];
+    const int d = static_cast<int>(p.c_ptr[x + 1] - pb);
+    const int64_t gx = p.g[x];
+    TopK<KPL> top;
+    top.init(p.k);
+    double tau_sh = -1.0;   // best k-th score of the workgroup, two stages old
+    int n = 0;              // stages done in this row (selects buffer / tau slot)
+
+    if (d > 0 && d <= kWave) {
+      // ---- stages in ascending g.  The two accumulator buffers alternate, so
+      // a wave that finished scanning stage n goes straight on to stage n+1's
+      // loads and adds while the others still scan: one barrier per stage.
+      Window w;
+      w.tw = 0;
+      w.v = 0; w.c = 0;
+      w.lo = w.hi = w.mx = w.hi1 = w.mx1 = 0;
+      if (lane < d) {
+        w.v = p.c_col[pb + lane];
+        w.c = p.c_val[pb + lane];
+        const int64_t vb = static_cast<int64_t>(w.v) * p.T;
+        w.lo = p.tile_off[vb];
+        w.hi = p.tile_off[vb + 1];
+        w.mx = p.tile_maxc[vb];
+        if (p.T > 1) { w.hi1 = p.tile_off[vb + 2]; w.mx1 = p.tile_maxc[vb + 1]; }
+      }
+      Stage cur;
+      bool have = find_stage(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, cur);
+      while (have) {
+        uint32_t* acc = lds + (n & 1) * nbuf;
+        for (int b = 0; b < cur.nb; ++b) {
+          Batch B;
+          issue(cur, b, p.tile_ent, wave, lane, B, no_add);
+          scatter(B, cur, acc, p.shift);
+        }
+        __syncthreads();
+        if (n >= 1) {
+          double tm = tau_s[(n - 1) & 1][0];
+#pragma unroll
+          for (int i = 1; i < kNW; ++i) tm = tau_s[(n - 1) & 1][i] > tm ? tau_s[(n - 1) & 1][i] : tm;
+          tau_sh = tm;
+        }
+        epilogue<KPL>(p, acc, top, Q, cur, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh);
+        // stage end: score what is queued while the wave's list is filling or
+        // the queue is half full; otherwise let it ride (one round trip per 64)
+        if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
+          flush<KPL>(p, Q, top, Q.n, gx, tau_sh, lane);
+        if (lane == 0) tau_s[n & 1][wave] = top.full() ? top.kth_s : -1.0;
+        ++n;
+        if (cur.pass + 1 < (1 << cur.lnp)) ++cur.pass;
+        else have = find_stage(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, cur);
+      }
+    } else if (d > kWave) {
+      // ---- rows with more than 64 venues: the same stages, synchronously
+      for (int64_t t = 0; t < p.T; ++t) {
+        int64_t ub = 0;
+        for (int g0 = 0; g0 < d; g0 += kWave) {
+          const int j = g0 + lane;
+          if (j < d)
+            ub += static_cast<int64_t>(p.c_val[pb + j]) *
+                  p.tile_maxc[static_cast<int64_t>(p.c_col[pb + j]) * p.T + t];
+        }
+        ub = wave_sum(ub);
+        if (!p.use_bounds) ub = int64_t(1) << 40;
+        if (ub == 0) continue;
+        if (tau_sh > 0.0 && ub < compute_mneed(tau_sh, gx + p.tile_gmin[t])) continue;
+        Stage S;
+        S.t = t;
+        S.lnp = ub <= 0xFF ? 0 : ub <= 0xFFFF ? 1 : 2;
+        S.gq = p.g_t[min((t << p.shift) + (static_cast<int64_t>(lane) << seg_shift),
+                         p.n_targets - 1)];
+        for (S.pass = 0; S.pass < (1 << S.lnp); ++S.pass) {
+          uint32_t* acc = lds + (n & 1) * nbuf;
+          for (int g0 = 0; !no_scatter && g0 < d; g0 += kWave) {
+            const int j = g0 + lane;
+            uint32_t lo = 0, hi = 0;
+            int c = 0;
+            if (j < d) {
+              const int64_t bk = static_cast<int64_t>(p.c_col[pb + j]) * p.T + t;
+              lo = p.tile_off[bk];
+              hi = p.tile_off[bk + 1];
+              c = p.c_val[pb + j];
+            }
+            grp_set(S.G, lo, hi, c, d - g0 < kWave ? d - g0 : kWave);
+            S.nb = (S.G.nq + kTB * kU - 1) / (kTB * kU);
+            for (int b = 0; b < S.nb; ++b) {
+              Batch B;
+              issue(S, b, p.tile_ent, wave, lane, B, no_add);
+              scatter(B, S, acc, p.shift);
+            }
+          }
+          __syncthreads();
+          if (n >= 1) {
+            double tm = tau_s[(n - 1) & 1][0];
+#pragma unroll
+            for (int i = 1; i < kNW; ++i) tm = tau_s[(n - 1) & 1][i] > tm ? tau_s[(n - 1) & 1][i] : tm;
+            tau_sh = tm;
+          }
+          epilogue<KPL>(p, acc, top, Q, S, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh);
+          if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
+            flush<KPL>(p, Q, top, Q.n, gx, tau_sh, lane);
+          if (lane == 0) tau_s[n & 1][wave] = top.full() ? top.kth_s : -1.0;
+          ++n;
+        }
+      }
+    }
+    if (Q.n > 0) flush<KPL>(p, Q, top, Q.n, gx, tau_sh, lane);
+    __syncthreads();   // every wave has finished scanning (and zeroing) its last stage
+
+    // ---- merge the four wave lists (the accumulators are all zero; reuse) ---
+    double* ms = reinterpret_cast<double*>(lds);          // [kNW][k]
+    int* my = reinterpret_cast<int*>(ms + kNW * p.k);     // [kNW][k]
+    int* mm = my + kNW * p.k;                              // [kNW][k]
+#pragma unroll
+    for (int q = 0; q < KPL; ++q) {
+      const int slot = q * kWave + lane;
+      if (slot < top.filled) {
+        ms[wave * p.k + slot] = top.s[q];
+        my[wave * p.k + slot] = top.y[q];
+        mm[wave * p.k + slot] = top.m[q];
+      }
+    }
+    if (lane == 0) fill_s[wave] = top.filled;
+    __syncthreads();
+    if (wave == 0) {
+      for (int w = 1; w < kNW; ++w) {
+        const int nf = fill_s[w];
+        for (int i = 0; i < nf; ++i) {
+          const double cs = ms[w * p.k + i];
+          const int cy = my[w * p.k + i];
+          if (!better(cs, cy, top.kth_s, top.kth_y)) break;   // lists are sorted
+          top.insert(cs, cy, mm[w * p.k + i]);
+        }
+      }
+      // ranked entries, then zero-score targets in reference order, then -1
+      int32_t* oi = p.out_idx + r * p.k;
+      int64_t* oc = p.out_cnt + r * p.k;
+      double* os = p.out_score + r * p.k;
+#pragma unroll
+      for (int q = 0; q < KPL; ++q) {
+        const int slot = q * kWave + lane;
+        if (slot < top.filled) { oi[slot] = top.y[q]; oc[slot] = top.m[q]; os[slot] = top.s[q]; }
+      }
+      const int64_t avail = p.n_targets - 1;
+      const int want = static_cast<int>(avail < p.k ? avail : p.k);
+      int slot = top.filled;
+      for (int64_t yb = 0; slot < want && yb < p.n_targets; yb += kWave) {
+        const int64_t yc = yb + lane;
+        bool ok = yc < p.n_targets && yc != x;
+        for (int q = 0; q < KPL; ++q) {
+          for (int l = 0; l < kWave; ++l) {
+            if (q * kWave + l >= top.filled) break;
+            ok = ok && (readlane(top.y[q], l) != static_cast<int>(yc));
+          }
+        }
+        const uint64_t mk = ballot(ok);
+        const int rank = mbcnt(mk);
+        if (ok && slot + rank < want) {
+          oi[slot + rank] = static_cast<int32_t>(yc);
+          oc[slot + rank] = 0;
+          os[slot + rank] = 0.0;
+        }
+        slot += __popcll(mk);
+      }
+      for (int s2 = want + lane; s2 < p.k; s2 += kWave) {
+        oi[s2] = -1;
+        oc[s2] = 0;
+        os[s2] = 0.0;
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < kNW * p.k * 4; i += kTB) lds[i] = 0;   // 16 B per merge entry
+  }
+}
+
+int log2_exact(int32_t w) {
+  int s = 0;
+  while (s < 31 && (1 << s) < w) ++s;
+  return (1 << s) == w ? s : -1;
+}
+
+template <int KPL>
+int launch(const CctParams& p, hipStream_t st) {
+  // two stage buffers of W/4 dwords; the row-end merge reuses them (16 B per entry)
+  int acc_dw = 2 * (1 << (p.shift - 2));
+  if (acc_dw < 4 * kNW * p.k) acc_dw = 4 * kNW * p.k;
+  const size_t lds = (static_cast<size_t>(acc_dw) + kNW * 2 * kQ) * sizeof(uint32_t);
+  DPS_HIP_RET(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cct_topk<KPL>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(lds)));
+  int dev = 0, n_cu = 256;
+  DPS_HIP_RET(hipGetDevice(&dev));
+  DPS_HIP_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  int per_cu = static_cast<int>((160 * 1024) / (lds + 256));
+  if (per_cu < 1) per_cu = 1;
+  if (per_cu > 8) per_cu = 8;   // 32 waves per CU
+  int64_t grid = static_cast<int64_t>(n_cu) * per_cu;
+  if (grid > p.n_rows) grid = p.n_rows;
+  k_cct_topk<KPL><<<static_cast<unsigned>(grid), kTB, lds, st>>>(p, acc_dw);
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+}  // namespace
+}  // namespace dps
+
+using namespace dps;
+
+extern "C" {
+
+size_t dps_cct_topk_workspace_size(void) { return 256; }
+
+int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                 const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
+                 const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                 const uint32_t* tile_off, const uint32_t* tile_ent, const uint32_t* tile_maxc,
+                 const int64_t* tile_gmin, int64_t row_begin, int64_t row_end, int32_t k,
+                 int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
+                 size_t ws_bytes, void* stream) {
+  (void)n_mids;
+  const int shift = log2_exact(tile_w);
+  DPS_REQUIRE(shift >= 8 && shift <= 14, DPS_ERR_UNSUPPORTED,
+              "tile_w must be a power of two in [256, 16384], got %d", tile_w);
+  DPS_REQUIRE(k >= 1 && k <= 256, DPS_ERR_UNSUPPORTED, "k must be in [1, 256], got %d", k);
+  DPS_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= n_targets, DPS_ERR_INVALID,
+              "row range [%lld, %lld) outside [0, %lld)", static_cast<long long>(row_begin),
+              static_cast<long long>(row_end), static_cast<long long>(n_targets));
+  DPS_REQUIRE(n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "n_targets exceeds int32");
+  DPS_REQUIRE(!t_perm == !t_rank, DPS_ERR_INVALID, "t_perm and t_rank go together");
+  DPS_REQUIRE(tile_gmin && g && tile_off && tile_ent, DPS_ERR_INVALID,
+              "g, tile_off, tile_ent and tile_gmin are required");
+  DPS_REQUIRE(ws && ws_bytes >= dps_cct_topk_workspace_size(), DPS_ERR_WORKSPACE,
+              "cct_topk workspace too small");
+  auto st = static_cast<hipStream_t>(stream);
+  const int64_t n_rows = row_end - row_begin;
+  if (n_rows == 0) return DPS_OK;
+  CctParams p;
+  p.c_ptr = c_ptr; p.c_col = c_col; p.c_val = c_val;
+  p.g = g; p.g_t = g_t ? g_t : g; p.t_perm = t_perm; p.t_rank = t_rank;
+  p.tile_off = tile_off; p.tile_ent = tile_ent; p.tile_gmin = tile_gmin;
+  p.tile_maxc = tile_maxc ? tile_maxc : tile_off;
+  p.use_bounds = tile_maxc != nullptr;
+  p.n_targets = n_targets;
+  p.T = (n_targets + tile_w - 1) / tile_w;
+  p.shift = shift;
+  p.row_begin = row_begin; p.n_rows = n_rows; p.k = k;
+  p.out_idx = out_idx; p.out_cnt = out_cnt; p.out_score = out_score;
+  p.counter = static_cast<unsigned long long*>(ws);
+  p.ablate = 0;
+  if (const char* ab = std::getenv("DPATHSIM_ABLATE")) p.ablate = std::atoi(ab);
+  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 8) ? 64 : sizeof(unsigned long long), st));
+  if (k <= 64) return launch<1>(p, st);
+  if (k <= 128) return launch<2>(p, st);
+  return launch<4>(p, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,332 @@
+// Operand layout for the hot kernel (dps_cct.hip) and the single-source
+// helpers of the reference-compatible class:
+//   dps_target_order   targets relabeled in ascending global walk g (stable
+//                      LSD radix sort) -- a pure layout choice;
+//   dps_ct_tiles_build C^T cut into target tiles of W = 2^shift labels, bucket
+//                      (v,t) = packed uint32 (C[y,v] << 16) | (label - t*W),
+//                      buckets [v][t], zero-padded to 16 bytes; per-bucket max
+//                      C and per-tile min g for the hot kernel's bounds;
+//   dps_walk_row / dps_row_scores / dps_pair_count: one source row, as the
+//                      reference's run() loop computes it (:30-52).
+#include "dps_common.hpp"
+
+namespace dps {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+// --------------------------------------------------------------------------
+// Target relabeling: ascending global walk g (ties: original index).  Tiles of
+// consecutive labels then hold targets of near-equal g, so a per-tile lower
+// bound gmin_t on g[y] makes the score filter almost exact.
+__global__ __launch_bounds__(kBlock) void k_invert_perm(const uint32_t* __restrict__ perm,
+                                                        int64_t n, int32_t* __restrict__ rank) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kBlock)
+    rank[perm[i]] = static_cast<int32_t>(i);
+}
+
+// --------------------------------------------------------------------------
+// Tile build: counting sort of C entries into (v, t) buckets, t = label >> shift.
+__device__ __forceinline__ int64_t label_of(const int32_t* rank, int64_t y) {
+  return rank ? static_cast<int64_t>(rank[y]) : y;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict__ c_ptr,
+                                                       const int32_t* __restrict__ c_col,
+                                                       const int32_t* __restrict__ c_val,
+                                                       const int32_t* __restrict__ rank,
+                                                       const int64_t* __restrict__ g,
+                                                       int64_t n_rows, int shift, int64_t T,
+                                                       uint32_t* __restrict__ cnt,
+                                                       uint32_t* __restrict__ maxc,
+                                                       unsigned long long* __restrict__ gmin,
+                                                       int32_t* __restrict__ status) {
+  const int lane = lane_id();
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  for (int64_t y = wave0; y < n_rows; y += nwaves) {
+    const int64_t t = label_of(rank, y) >> shift;
+    if (lane == 0 && gmin) atomicMin(&gmin[t], static_cast<unsigned long long>(g[y]));
+    for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
+      const int32_t c = c_val[j];
+      if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
+      const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
+      atomicAdd(&cnt[b], 1u);
+      if (maxc) atomicMax(&maxc[b], static_cast<uint32_t>(c));
+    }
+  }
+}
+
+// Buckets are padded to a multiple of 4 entries (16 B) so the hot kernel's
+// 16-byte chunks never straddle two buckets; padding entries are 0 (C = 0).
+__global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, int64_t n) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kBlock)
+    cnt[i] = (cnt[i] + 3u) & ~3u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ cursor,
+                                                     int64_t n, uint32_t* __restrict__ ent) {
+  for (int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; b < n;
+       b += static_cast<int64_t>(gridDim.x) * kBlock)
+    for (int64_t i = off[b] + cursor[b]; i < off[b + 1]; ++i) ent[i] = 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_off32(const int64_t* __restrict__ p64,
+                                                       int64_t n, uint32_t* __restrict__ p32) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i <= n;
+       i += static_cast<int64_t>(gridDim.x) * kBlock)
+    p32[i] = static_cast<uint32_t>(p64[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restrict__ c_ptr,
+                                                         const int32_t* __restrict__ c_col,
+                                                         const int32_t* __restrict__ c_val,
+                                                         const int32_t* __restrict__ rank,
+                                                         int64_t n_rows, int shift, int64_t T,
+                                                         const int64_t* __restrict__ off,
+                                                         uint32_t* __restrict__ cursor,
+                                                         uint32_t* __restrict__ ent) {
+  const int lane = lane_id();
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  const uint32_t ymask = (1u << shift) - 1u;
+  for (int64_t y = wave0; y < n_rows; y += nwaves) {
+    const int64_t lab = label_of(rank, y);
+    const int64_t t = lab >> shift;
+    for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
+      const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
+      const uint32_t pos = atomicAdd(&cursor[b], 1u);
+      ent[off[b] + pos] =
+          (static_cast<uint32_t>(c_val[j]) << 16) | (static_cast<uint32_t>(lab) & ymask);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+// Single-source dense row: one block per target tile; out_m in ORIGINAL order.
+__global__ __launch_bounds__(kBlock) void k_walk_row(const int32_t* __restrict__ src_col,
+                                                     const int32_t* __restrict__ src_val,
+                                                     int64_t src_len, int64_t n_targets, int shift,
+                                                     int64_t T, const uint32_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ ent,
+                                                     const int32_t* __restrict__ t_perm,
+                                                     int64_t* __restrict__ out_m) {
+  extern __shared__ __attribute__((aligned(16))) int32_t acc[];
+  const int W = 1 << shift;
+  const int64_t t = blockIdx.x;
+  for (int i = threadIdx.x; i < W; i += kBlock) acc[i] = 0;
+  __syncthreads();
+  for (int64_t j = 0; j < src_len; ++j) {
+    const int64_t b = static_cast<int64_t>(src_col[j]) * T + t;
+    const int cx = src_val[j];
+    for (uint32_t i = off[b] + threadIdx.x; i < off[b + 1]; i += kBlock) {
+      const uint32_t e = ent[i];
+      atomicAdd(&acc[e & 0xFFFFu], cx * static_cast<int>(e >> 16));
+    }
+  }
+  __syncthreads();
+  const int64_t y0 = t << shift;
+  for (int i = threadIdx.x; i < W && y0 + i < n_targets; i += kBlock) {
+    const int64_t lab = y0 + i;
+    out_m[t_perm ? t_perm[lab] : lab] = acc[i];
+  }
+}
+
+// score[y] = (double)(2*m[y]) / (double)(gx + g[y]) -- the reference's :51-52
+// for one source row; *zero_div = number of targets with gx + g[y] == 0
+// (the reference raises ZeroDivisionError there; score is left 0.0).
+__global__ __launch_bounds__(kBlock) void k_row_scores(const int64_t* __restrict__ m,
+                                                       const int64_t* __restrict__ g, int64_t gx,
+                                                       int64_t n, double* __restrict__ score,
+                                                       unsigned long long* zero_div) {
+  for (int64_t y = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; y < n;
+       y += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int64_t den = gx + g[y];
+    if (den == 0) {
+      score[y] = 0.0;
+      if (zero_div) atomicAdd(zero_div, 1ull);
+    } else {
+      score[y] = static_cast<double>(2 * m[y]) / static_cast<double>(den);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kWave) void k_pair_count(const int32_t* __restrict__ a_col,
+                                                      const int32_t* __restrict__ a_val,
+                                                      int64_t a_len,
+                                                      const int32_t* __restrict__ b_col,
+                                                      const int32_t* __restrict__ b_val,
+                                                      int64_t b_len, int64_t* out) {
+  int64_t sum = 0;
+  for (int64_t i = threadIdx.x; i < a_len; i += kWave) {
+    const int32_t v = a_col[i];
+    int64_t lo = 0, hi = b_len;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (b_col[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    if (lo < b_len && b_col[lo] == v) sum += static_cast<int64_t>(a_val[i]) * b_val[lo];
+  }
+  sum = wave_sum(sum);
+  if (threadIdx.x == 0) *out = sum;
+}
+
+int log2_exact(int32_t w) {
+  int s = 0;
+  while (s < 31 && (1 << s) < w) ++s;
+  return (1 << s) == w ? s : -1;
+}
+
+}  // namespace
+}  // namespace dps
+
+using namespace dps;
+
+
+extern "C" {
+
+size_t dps_target_order_workspace_size(int64_t n_targets) {
+  return radix_sort_workspace_size(n_targets);
+}
+
+int dps_target_order(const int64_t* g, int64_t n_targets, int32_t key_bits, int32_t* t_perm,
+                     int32_t* t_rank, int64_t* g_t, void* ws, size_t ws_bytes, void* stream) {
+  DPS_REQUIRE(n_targets >= 0 && n_targets < INT32_MAX, DPS_ERR_INVALID, "bad n_targets");
+  DPS_REQUIRE(key_bits >= 1 && key_bits <= 64, DPS_ERR_INVALID, "key_bits must be in [1,64]");
+  DPS_REQUIRE(ws_bytes >= dps_target_order_workspace_size(n_targets), DPS_ERR_WORKSPACE,
+              "target_order workspace too small");
+  auto st = static_cast<hipStream_t>(stream);
+  if (n_targets == 0) return DPS_OK;
+  DPS_HIP_RET(radix_sort_pairs(reinterpret_cast<const uint64_t*>(g), nullptr,
+                               reinterpret_cast<uint64_t*>(g_t),
+                               reinterpret_cast<uint32_t*>(t_perm), n_targets, key_bits, ws,
+                               ws_bytes, st));
+  k_invert_perm<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(
+      reinterpret_cast<const uint32_t*>(t_perm), n_targets, t_rank);
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+int64_t dps_ct_tiles_ent_capacity(int64_t nnz, int64_t n_mids, int64_t n_targets,
+                                  int32_t tile_w) {
+  if (tile_w <= 0) return 0;
+  const int64_t T = (n_targets + tile_w - 1) / tile_w;
+  const int64_t nb = n_mids * (T > 0 ? T : 1);
+  return nnz + 3 * (nb < nnz ? nb : nnz) + 4;
+}
+
+size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t tile_w) {
+  if (tile_w <= 0) return 0;
+  const int64_t T = (n_targets + tile_w - 1) / tile_w;
+  const int64_t nb = n_mids * (T > 0 ? T : 1);
+  size_t s = 0;
+  s += align_up(static_cast<size_t>(nb + 1) * sizeof(uint32_t));  // cnt
+  s += align_up(static_cast<size_t>(nb + 1) * sizeof(uint32_t));  // cursor
+  s += align_up(static_cast<size_t>(nb + 1) * sizeof(int64_t));   // off64
+  s += align_up(scan_workspace_size(nb + 1));
+  return s + 1024;
+}
+
+int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                       const int64_t* g, const int32_t* t_rank, int64_t n_targets, int64_t n_mids,
+                       int32_t tile_w, uint32_t* tile_off, uint32_t* tile_ent, uint32_t* tile_maxc,
+                       int64_t* tile_gmin, int32_t* status_dev, void* ws, size_t ws_bytes,
+                       void* stream) {
+  const int shift = log2_exact(tile_w);
+  DPS_REQUIRE(shift >= 8 && shift <= 14, DPS_ERR_UNSUPPORTED,
+              "tile_w must be a power of two in [256, 16384], got %d", tile_w);
+  DPS_REQUIRE(n_targets >= 0 && n_mids >= 0, DPS_ERR_INVALID, "negative size");
+  DPS_REQUIRE(n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "n_targets exceeds int32");
+  DPS_REQUIRE(!tile_gmin || g, DPS_ERR_INVALID, "tile_gmin needs g");
+  DPS_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 256 == 0, DPS_ERR_WORKSPACE,
+              "workspace not 256-byte aligned");
+  DPS_REQUIRE(ws_bytes >= dps_ct_tiles_workspace_size(n_mids, n_targets, tile_w),
+              DPS_ERR_WORKSPACE, "tiles workspace too small");
+  auto st = static_cast<hipStream_t>(stream);
+  const int64_t T = (n_targets + tile_w - 1) / tile_w;
+  const int64_t nb = n_mids * T;
+  Carve c(ws, ws_bytes);
+  uint32_t* cnt = c.take<uint32_t>(nb + 1);
+  uint32_t* cursor = c.take<uint32_t>(nb + 1);
+  int64_t* off64 = c.take<int64_t>(nb + 1);
+  const size_t scan_ws = scan_workspace_size(nb + 1);
+  void* sws = c.take<char>(scan_ws);
+  DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "tiles workspace carve failed");
+  if (status_dev) DPS_HIP_RET(hipMemsetAsync(status_dev, 0, sizeof(int32_t), st));
+  DPS_HIP_RET(hipMemsetAsync(cnt, 0, (nb + 1) * sizeof(uint32_t), st));
+  DPS_HIP_RET(hipMemsetAsync(cursor, 0, (nb + 1) * sizeof(uint32_t), st));
+  if (tile_maxc) DPS_HIP_RET(hipMemsetAsync(tile_maxc, 0, (nb + 1) * sizeof(uint32_t), st));
+  if (tile_gmin && T > 0) DPS_HIP_RET(hipMemsetAsync(tile_gmin, 0x7F, T * sizeof(int64_t), st));
+  if (n_targets > 0 && nb > 0) {
+    k_tile_count<<<grid_for(n_targets * kWave, kBlock), kBlock, 0, st>>>(
+        c_ptr, c_col, c_val, t_rank, g, n_targets, shift, T, cnt, tile_maxc,
+        reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
+    DPS_LAUNCHED();
+  }
+  if (nb > 0) {
+    k_round4<<<grid_for(nb, kBlock), kBlock, 0, st>>>(cnt, nb);
+    DPS_LAUNCHED();
+  }
+  DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, off64, nb, sws, scan_ws, st));
+  k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, nb, tile_off);
+  DPS_LAUNCHED();
+  if (n_targets > 0 && nb > 0) {
+    k_tile_scatter<<<grid_for(n_targets * kWave, kBlock), kBlock, 0, st>>>(
+        c_ptr, c_col, c_val, t_rank, n_targets, shift, T, off64, cursor, tile_ent);
+    DPS_LAUNCHED();
+  }
+  if (nb > 0) {
+    k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(off64, cursor, nb, tile_ent);
+    DPS_LAUNCHED();
+  }
+  return DPS_OK;
+}
+
+int dps_walk_row(const int32_t* src_col, const int32_t* src_val, int64_t src_len,
+                 const int32_t* t_perm, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                 const uint32_t* tile_off, const uint32_t* tile_ent, int64_t* out_m,
+                 void* stream) {
+  (void)n_mids;
+  const int shift = log2_exact(tile_w);
+  DPS_REQUIRE(shift >= 8 && shift <= 14, DPS_ERR_UNSUPPORTED, "bad tile_w %d", tile_w);
+  DPS_REQUIRE(src_len >= 0 && n_targets >= 0, DPS_ERR_INVALID, "negative size");
+  auto st = static_cast<hipStream_t>(stream);
+  const int64_t T = (n_targets + tile_w - 1) / tile_w;
+  if (T == 0) return DPS_OK;
+  DPS_HIP_RET(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_walk_row),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(tile_w * sizeof(int32_t))));
+  k_walk_row<<<static_cast<unsigned>(T), kBlock, static_cast<size_t>(tile_w) * sizeof(int32_t),
+               st>>>(src_col, src_val, src_len, n_targets, shift, T, tile_off, tile_ent, t_perm,
+                     out_m);
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+int dps_row_scores(const int64_t* m, const int64_t* g, int64_t gx, int64_t n, double* score,
+                   int64_t* zero_div, void* stream) {
+  DPS_REQUIRE(n >= 0 && gx >= 0, DPS_ERR_INVALID, "bad arguments");
+  auto st = static_cast<hipStream_t>(stream);
+  if (zero_div) DPS_HIP_RET(hipMemsetAsync(zero_div, 0, sizeof(int64_t), st));
+  if (n == 0) return DPS_OK;
+  k_row_scores<<<grid_for(n, kBlock), kBlock, 0, st>>>(
+      m, g, gx, n, score, reinterpret_cast<unsigned long long*>(zero_div));
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+int dps_pair_count(const int32_t* a_col, const int32_t* a_val, int64_t a_len,
+                   const int32_t* b_col, const int32_t* b_val, int64_t b_len, int64_t* out,
+                   void* stream) {
+  DPS_REQUIRE(a_len >= 0 && b_len >= 0 && out, DPS_ERR_INVALID, "bad arguments");
+  auto st = static_cast<hipStream_t>(stream);
+  k_pair_count<<<1, kWave, 0, st>>>(a_col, a_val, a_len, b_col, b_val, b_len, out);
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+}  // extern "C"

@@ -16,7 +16,7 @@ import torch
 from . import _lib
 from .graph import TypedTables
 
-DEFAULT_TILE_W = 4096
+DEFAULT_TILE_W = 16384
 
 
 def _ptr(t):
@@ -173,11 +173,12 @@ class PathSimEngine:
             tile_off = self._empty(NV * T + 1, torch.int32)
             tile_maxc = self._empty(NV * T + 1, torch.int32)
             tile_gmin = self._empty(T, torch.int64)
-            tile_ent = self._empty(nnz_c + 4, torch.int32)   # +16 B: kernel reads whole 16-B chunks
+            ent_cap = _lib.size("dps_ct_tiles_ent_capacity", nnz_c, NV, NA, self.tile_w)
+            if ent_cap >= 2 ** 32:
+                raise OverflowError("padded nnz(C) >= 2^32 exceeds the uint32 tile offsets")
+            tile_ent = self._empty(ent_cap, torch.int32)
             status = self._empty(1, torch.int32)
             tws = self._ws(_lib.size("dps_ct_tiles_workspace_size", NV, NA, self.tile_w))
-            if nnz_c >= 2 ** 32:
-                raise OverflowError("nnz(C) >= 2^32 exceeds the uint32 tile offsets")
             _lib.call("dps_ct_tiles_build", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(g),
                       _ptr(t_rank), NA, NV, self.tile_w, _ptr(tile_off), _ptr(tile_ent),
                       _ptr(tile_maxc), _ptr(tile_gmin), _ptr(status), _ptr(tws), tws.numel(), st)
