@@ -42,8 +42,8 @@ def parse():
     ap.add_argument("--tile-w", type=int, default=16384)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", default=None,
-                    help="rocprofv3 PMC summary (profiles/...) to fill roofline.traffic")
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01", "pmc_hot.json"),
+                    help="rocprofv3 PMC summary of the hot kernel (tools/pmc.sh) for roofline.traffic")
     return ap.parse_args()
 
 
@@ -53,6 +53,7 @@ def main():
     import torch
     import torch.distributed as dist
 
+    from dpathsim.dist import gather_topk, max_shard, shard_bounds
     from dpathsim.engine import PathSimEngine
     from dpathsim.synth import CONFIGS, synth_config
 
@@ -72,17 +73,15 @@ def main():
     NA = typed.n_authors
 
     eng = PathSimEngine(typed, device=dev, tile_w=args.tile_w).upload()
-    # balanced contiguous row shards
-    r0 = NA * rank // world
-    r1 = NA * (rank + 1) // world
+    r0, r1 = shard_bounds(NA, rank, world)       # contiguous balanced row shard
     shard = r1 - r0
-    max_shard = max(NA * (r + 1) // world - NA * r // world for r in range(world))
-    out = (torch.empty((max_shard, k), dtype=torch.int32, device=dev),
-           torch.empty((max_shard, k), dtype=torch.int64, device=dev),
-           torch.empty((max_shard, k), dtype=torch.float64, device=dev))
+    m = max_shard(NA, world)
+    out = (torch.empty((m, k), dtype=torch.int32, device=dev),
+           torch.empty((m, k), dtype=torch.int64, device=dev),
+           torch.empty((m, k), dtype=torch.float64, device=dev))
     gathered = None
     if world > 1:
-        gathered = tuple(torch.empty((world * max_shard, k), dtype=t.dtype, device=dev) for t in out)
+        gathered = tuple(torch.empty((world * m, k), dtype=t.dtype, device=dev) for t in out)
 
     ev_topk = []
 
@@ -98,8 +97,7 @@ def main():
             e1.record()
             ev_topk.append((e0, e1))
         if world > 1:
-            for src, dst in zip(out, gathered):
-                dist.all_gather_into_tensor(dst, src)
+            gather_topk(out, NA, world, out=gathered)
 
     for _ in range(args.warmup):
         step(False)
@@ -138,7 +136,8 @@ def main():
     if args.pmc_json and os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
-            if pm.get("config") == args.config and pm.get("world") == world:
+            if (pm.get("config") == args.config and pm.get("world") == world
+                    and pm.get("tile_w", args.tile_w) == args.tile_w and args.scale == 1.0):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -153,14 +152,15 @@ def main():
             threads = os.cpu_count() or 1
             threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
             co = po.COracle.from_typed(typed)
-            probe = 256
-            t1 = time.perf_counter()
-            co.topk(k, 0, probe, threads=threads)
-            dt = time.perf_counter() - t1
-            rows = int(min(NA, max(probe, probe * args.cpu_baseline_seconds / max(dt, 1e-3))))
-            t1 = time.perf_counter()
-            co.topk(k, 0, rows, threads=threads)
-            dt = time.perf_counter() - t1
+            co.topk(k, 0, 64, threads=threads)          # warm-up: per-thread accumulators
+            rows, dt, chunk = 0, 0.0, 256
+            while dt < args.cpu_baseline_seconds and rows < NA:   # doubling row blocks
+                n = min(chunk, NA - rows)
+                t1 = time.perf_counter()
+                co.topk(k, rows, rows + n, threads=threads)
+                dt += time.perf_counter() - t1
+                rows += n
+                chunk *= 2
             cpu = {"value": rows * (NA - 1) / dt, "unit": "pairs/s", "cores": threads,
                    "kind": "port",
                    "sample": f"oracle/pathsim_oracle.c (OpenMP), author rows [0,{rows}) x all "

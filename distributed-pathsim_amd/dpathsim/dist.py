@@ -1,0 +1,50 @@
+"""Row sharding of the all-pairs top-k across ranks.
+
+Every source row's top-k depends only on that row of C plus all of C and g,
+so ranks split the author rows into contiguous, balanced shards and exchange
+nothing but the finished top-k blocks.  One process per GPU; the collective is
+RCCL (``nccl`` backend) on the GPU box and gloo in the CPU tests.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n_rows: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous balanced shard [r0, r1) of rank ``rank`` out of ``world``."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} / world {world}")
+    return n_rows * rank // world, n_rows * (rank + 1) // world
+
+
+def max_shard(n_rows: int, world: int) -> int:
+    return max(b - a for a, b in (shard_bounds(n_rows, r, world) for r in range(world)))
+
+
+def gather_topk(parts, n_rows: int, world: int, group=None, out=None):
+    """All-gather every rank's top-k block into the full [n_rows, k] tensors.
+
+    ``parts``: this rank's (idx, cnt, score) tensors with shape [max_shard, k]
+    (rows past its shard are padding).  Returns (idx, cnt, score) for all
+    n_rows rows in row order on every rank; ``out`` may hold preallocated
+    [world * max_shard, k] receive buffers (reused across steps).
+    """
+    if world == 1:
+        r1 = shard_bounds(n_rows, 0, 1)[1]
+        return tuple(p[:r1] for p in parts)
+    m = max_shard(n_rows, world)
+    if out is None:
+        out = tuple(torch.empty((world * m,) + tuple(p.shape[1:]), dtype=p.dtype, device=p.device)
+                    for p in parts)
+    for src, dst in zip(parts, out):
+        if src.shape[0] != m:
+            raise ValueError(f"part has {src.shape[0]} rows, expected max_shard {m}")
+        if dist.get_backend(group) == "nccl":
+            dist.all_gather_into_tensor(dst, src.contiguous(), group=group)
+        else:
+            dist.all_gather(list(dst.view(world, m, *src.shape[1:]).unbind(0)), src.contiguous(),
+                            group=group)
+    rows = [slice(r * m, r * m + (b - a)) for r, (a, b) in
+            enumerate(shard_bounds(n_rows, r, world) for r in range(world))]
+    return tuple(torch.cat([o[s] for s in rows]) for o in out)

@@ -1,0 +1,69 @@
+"""Multi-rank row sharding + top-k gather (dpathsim.dist) on CPU with gloo.
+
+The GPU path runs the same code with the nccl (RCCL) backend in bench.py; here
+the per-shard top-k comes from the C oracle so the test needs no GPU.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dpathsim.dist import gather_topk, max_shard, shard_bounds
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 1000, 1_000_003])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shards_partition_rows(n, world):
+    bounds = [shard_bounds(n, r, world) for r in range(world)]
+    assert bounds[0][0] == 0 and bounds[-1][1] == n
+    for (a, b), (c, _) in zip(bounds, bounds[1:]):
+        assert b == c and a <= b
+    sizes = [b - a for a, b in bounds]
+    assert max(sizes) - min(sizes) <= 1
+    assert max_shard(n, world) == max(sizes)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, k, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pathsim_oracle as po
+        from dpathsim.synth import synth_dblp
+        t = synth_dblp(1500, 4500, 120, seed=21).typed()
+        co = po.COracle.from_typed(t)
+        na = t.n_authors
+        r0, r1 = shard_bounds(na, rank, world)
+        m = max_shard(na, world)
+        oi, oc, os_ = co.topk(k, r0, r1, threads=1)
+        parts = []
+        for a, dt in ((oi, torch.int32), (oc, torch.int64), (os_, torch.float64)):
+            p = torch.zeros((m, k), dtype=dt)
+            p[: r1 - r0] = torch.from_numpy(a)
+            parts.append(p)
+        gi, gc, gs = gather_topk(tuple(parts), na, world)
+        if rank == 0:
+            fi, fc, fs = co.topk(k, 0, na, threads=1)
+            ok = (np.array_equal(gi.numpy(), fi) and np.array_equal(gc.numpy(), fc)
+                  and np.array_equal(gs.numpy().view(np.int64), fs.view(np.int64)))
+            with open(result_path, "w") as f:
+                f.write("ok" if ok else "mismatch")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_gather_equals_single_rank(tmp_path, world):
+    out = tmp_path / "result.txt"
+    mp.start_processes(_worker, args=(world, _free_port(), 10, str(out)), nprocs=world,
+                       join=True, start_method="spawn")
+    assert out.read_text() == "ok"
