@@ -172,7 +172,7 @@ def main():
 
     if rank == 0:
         rec = {
-            "metric": "PathSim pairs scored/sec (APVPA all-pairs top-k)",
+            "metric": f"PathSim pairs scored/sec ({mp_name} all-pairs top-k)",
             "value": value,
             "unit": "pairs/s",
             "n_gpus": world,

@@ -80,3 +80,29 @@ def test_config3_sample_rows():
     co = _oracle(t)
     _check(eng, co, 10, rows=(0, 1500))
     _check(eng, co, 10, rows=(777_000, 778_500))
+
+
+def test_config4_aptpa_sample_rows():
+    """Full-size config4 (APTPA, 200k topics, ~30 topics per row, rows > 64 topics
+    take the general path): two 1000-row slices vs the C oracle."""
+    from dpathsim.engine import build_engine
+    from dpathsim.graph import APTPA
+    from dpathsim.synth import synth_config
+    t = synth_config("config4").typed(APTPA)
+    eng = build_engine(t)
+    co = _oracle(t)
+    assert eng.info.nnz_c == len(co.export()[1])
+    _check(eng, co, 10, rows=(0, 1000))
+    _check(eng, co, 10, rows=(500_000, 501_000))
+
+
+def test_config5_k100_sample_rows():
+    """Full-size config5 (3M authors / 10M papers / 20k venues, top-100): two
+    400-row slices vs the C oracle."""
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_config
+    t = synth_config("config5").typed()
+    eng = build_engine(t)
+    co = _oracle(t)
+    _check(eng, co, 100, rows=(0, 400))
+    _check(eng, co, 100, rows=(2_999_600, 3_000_000))
