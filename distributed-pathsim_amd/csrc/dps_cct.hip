@@ -42,7 +42,6 @@ namespace {
 constexpr int kTB = 256;            // threads per workgroup
 constexpr int kNW = kTB / kWave;    // waves per workgroup
 constexpr int kU = 4;               // 16-B chunk loads in flight per lane
-constexpr int kSegs = kWave;        // threshold segments per tile (one per lane)
 constexpr int kQ = 2 * kWave;       // per-wave candidate queue (label, M) capacity
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -52,28 +51,19 @@ __device__ __forceinline__ bool better(double s1, int y1, double s2, int y2) {
   return s1 > s2 || (s1 == s2 && y1 < y2);
 }
 
-// Integer threshold: the smallest m >= 0 with fl(2m / den) >= kth.  Every
-// target y with g[y] >= g0 has gx + g[y] >= den := gx + g0, so (rounding is
-// monotone) fl(2M/(gx+g[y])) <= fl(2M/den), and m -> fl(2m/den) is
-// nondecreasing: a target with M < mneed scores strictly below kth and cannot
-// enter the top-k, ties included.  Starts one below ceil(kth*den/2), so it
-// usually settles after two divisions.
-__device__ __forceinline__ int compute_mneed(double kth, int64_t den) {
+// Integer threshold, conservative: a lower bound on the smallest m >= 0 with
+// fl(2m / den) >= kth.  Every target y with g[y] >= g0 has gx + g[y] >= den :=
+// gx + g0, so (rounding is monotone) fl(2M/(gx+g[y])) <= fl(2M/den), and
+// m -> fl(2m/den) is nondecreasing: a target with M below the exact threshold
+// m* scores strictly below kth and cannot enter the top-k, ties included.
+// fl(2m*/den) >= kth gives m* >= kth*den/2*(1 - 2^-53); the value below is
+// at most kth*den/2*(1 - 2^-50)*(1 + 2^-52) < that, so it never exceeds m*
+// (it is m* or m* - 1 in practice).  Two multiplies, no division.
+__device__ __forceinline__ int mneed_lo(double kth, int64_t den) {
   if (kth <= 0.0 || den <= 0) return 0;
-  const double dd = static_cast<double>(den);
-  const double r = kth * dd * 0.5;
+  const double r = kth * static_cast<double>(den) * (0.5 * (1.0 - 0x1p-50));
   if (r >= 2147483000.0) return INT32_MAX;
-  double m = ceil(r) - 1.0;               // integers below 2^31: 2m is exact
-  if (m < 0.0) m = 0.0;
-  if ((2.0 * m) / dd >= kth) {
-#pragma clang loop vectorize(disable) unroll(disable)
-    while (m > 0.0 && (2.0 * (m - 1.0)) / dd >= kth) m -= 1.0;
-  } else {
-    m += 1.0;
-#pragma clang loop vectorize(disable) unroll(disable)
-    while ((2.0 * m) / dd < kth) m += 1.0;
-  }
-  return static_cast<int>(m);
+  return static_cast<int>(r);   // truncation = floor for r >= 0
 }
 
 // Register-resident sorted top-k of one wave: rank r*64 + lane in slot r.
@@ -155,6 +145,7 @@ struct CctParams {
   int64_t* out_cnt;
   double* out_score;
   unsigned long long* counter;
+  bool dbuf;                 // two alternating stage buffers (W <= 16384) or one
   int ablate;                // profiling aid (DPATHSIM_ABLATE): 1 no LDS adds, 2 no
                              // candidate scoring, 4 no scatter
 };
@@ -168,10 +159,29 @@ struct Grp {
   int nv;        // venues in the group (wave-uniform, <= 64)
 };
 
+// wave64 inclusive prefix sum / total of a u32 with DPP row shifts and row
+// broadcasts (gfx9 DPP: no LDS round trips).  Lanes shifted in from outside a
+// row, or masked off by the row/bank masks, contribute 0.
+#define DPS_DPP(v, ctrl, rm, bm) \
+  static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), ctrl, rm, bm, false))
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t x) {
+  x += DPS_DPP(x, 0x111, 0xF, 0xF);   // row_shr:1
+  x += DPS_DPP(x, 0x112, 0xF, 0xF);   // row_shr:2
+  x += DPS_DPP(x, 0x114, 0xF, 0xE);   // row_shr:4
+  x += DPS_DPP(x, 0x118, 0xF, 0xC);   // row_shr:8
+  x += DPS_DPP(x, 0x142, 0xA, 0xF);   // row_bcast:15
+  x += DPS_DPP(x, 0x143, 0xC, 0xF);   // row_bcast:31
+  return x;
+}
+// Total over the wave (wave-uniform result).
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+  return static_cast<uint32_t>(readlane(static_cast<int>(wave_incl_sum_u32(x)), kWave - 1));
+}
+
 __device__ __forceinline__ void grp_set(Grp& G, uint32_t lo, uint32_t hi, int c, int nv) {
   G.c = c;
   const int nch = static_cast<int>((hi - lo) >> 2);
-  const int inc = wave_inclusive_sum(nch);
+  const int inc = static_cast<int>(wave_incl_sum_u32(static_cast<uint32_t>(nch)));
   G.pre = inc - nch;
   G.base = lo - 4u * static_cast<uint32_t>(G.pre);
   G.nq = readlane(inc, kWave - 1);
@@ -212,6 +222,7 @@ struct Stage {
   int lnp;       // log2(number of passes): 0 u8, 1 u16, 2 u32
   int pass;
   int nb;        // batches of kTB*kU chunks (0 under the no-scatter ablation)
+  int jc;        // venue cursor of issue(): venue of the last chunk block issued
   int64_t gq;    // lane s: smallest g of segment s of tile t
 };
 
@@ -221,20 +232,41 @@ struct Batch {
 };
 
 // Issue the loads of batch b of stage S: chunk q -> lane (q mod 256) of the
-// workgroup, kU chunks per lane.
-__device__ __forceinline__ void issue(const Stage& S, int b, const uint32_t* __restrict__ ent,
+// workgroup, kU chunks per lane.  Each load instruction reads 64 consecutive
+// chunks (q0 .. q0+63, q0 wave-uniform).  A wave-uniform venue cursor follows
+// the chunk blocks in order; when all 64 chunks of a load lie in the cursor's
+// venue (the common case: heavy venues own most chunks) the base address and
+// C[x,v] are scalars and the load costs a couple of VALU.  A load that straddles
+// venue boundaries resolves each lane's venue with chunk_venue().  Loads past
+// the stage's last chunk are skipped (uniform) and marked dead (c = 0).
+__device__ __forceinline__ void issue(Stage& S, int b, const uint32_t* __restrict__ ent,
                                       int wave, int lane, Batch& B, bool no_add) {
-  int sp[kSmallGroup];
-#pragma unroll
-  for (int jj = 0; jj < kSmallGroup; ++jj) sp[jj] = readlane(S.G.pre, jj);
-  const int q0 = b * (kTB * kU) + wave * kWave + lane;
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
-    const int q = q0 + u * kTB;
-    const int j = chunk_venue(S.G, sp, q);
-    const uint32_t bj = static_cast<uint32_t>(__shfl(static_cast<int>(S.G.base), j, kWave));
-    const int cj = __shfl(S.G.c, j, kWave);
+    const int q0 = b * (kTB * kU) + u * kTB + wave * kWave;   // wave-uniform
+    B.c[u] = 0;
+    B.e[u] = make_uint4(0, 0, 0, 0);
+    if (q0 >= S.G.nq) continue;
+    int jn = S.jc + 1 < S.G.nv ? readlane(S.G.pre, S.jc + 1) : INT_MAX;
+    while (q0 >= jn) {
+      ++S.jc;
+      jn = S.jc + 1 < S.G.nv ? readlane(S.G.pre, S.jc + 1) : INT_MAX;
+    }
+    const int q = q0 + lane;
     const bool live = q < S.G.nq;
+    uint32_t bj;
+    int cj;
+    if (q0 + kWave - 1 < jn) {
+      bj = readlane(S.G.base, S.jc);
+      cj = readlane(S.G.c, S.jc);
+    } else {
+      int sp[kSmallGroup];
+#pragma unroll
+      for (int jj = 0; jj < kSmallGroup; ++jj) sp[jj] = readlane(S.G.pre, jj);
+      const int j = chunk_venue(S.G, sp, q);
+      bj = static_cast<uint32_t>(__shfl(static_cast<int>(S.G.base), j, kWave));
+      cj = __shfl(S.G.c, j, kWave);
+    }
     B.e[u] = *reinterpret_cast<const uint4*>(ent + (live ? bj + 4u * static_cast<uint32_t>(q) : 0u));
     B.c[u] = live && !no_add ? cj : 0;
   }
@@ -273,6 +305,38 @@ __device__ __forceinline__ void scatter(const Batch& B, const Stage& S, uint32_t
     acc_add(acc, B.e[u].z, B.c[u], S.lnp, S.pass, shift);
     acc_add(acc, B.e[u].w, B.c[u], S.lnp, S.pass, shift);
   }
+}
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// u8 accumulation (UB <= 255): one LDS byte per target, four per dword.  The
+// entry's low 16 bits are the tile-local label: bits [2, shift) pick the dword,
+// bits [0, 2) the byte, so the LDS address is buf | (e & lab_mask) (buf is
+// W-aligned) and the byte shift is (e << 3) mod 32 -- five VALU per entry and no
+// branch.  Padding entries carry C = 0 (they add 0 to a spread-out dword).
+__device__ __forceinline__ void add_u8(uint32_t buf, uint32_t e, uint32_t c, uint32_t lab_mask) {
+  const uint32_t val = __umul24(c, e >> 16);
+  const uint32_t add = val << ((e << 3) & 31u);
+  __hip_atomic_fetch_add(reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(buf | (e & lab_mask))),
+                         add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void scatter_u8(const Batch& B, uint32_t buf, uint32_t lab_mask) {
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const uint32_t c = static_cast<uint32_t>(B.c[u]);
+    if (c == 0) continue;   // dead chunk (beyond the stage's last)
+    add_u8(buf, B.e[u].x, c, lab_mask);
+    add_u8(buf, B.e[u].y, c, lab_mask);
+    add_u8(buf, B.e[u].z, c, lab_mask);
+    add_u8(buf, B.e[u].w, c, lab_mask);
+  }
+}
+
+__device__ __forceinline__ void scatter_any(const Batch& B, const Stage& S, uint32_t* acc,
+                                            uint32_t buf, uint32_t lab_mask, int shift) {
+  if (S.lnp == 0) scatter_u8(B, buf, lab_mask);
+  else scatter(B, S, acc, shift);
 }
 
 __device__ __forceinline__ void wave_lds_fence() {
@@ -348,19 +412,103 @@ __device__ __forceinline__ bool block_any(uint4 a, uint32_t m, int lnp) {
   return max(max(a.x, a.y), max(a.z, a.w)) >= m;
 }
 
+// Per-byte flags (bit 7 of each byte) of a packed u8 dword: byte >= m, exact
+// for 1 <= m <= 255 (no carry crosses a byte: low7 + 128 - m <= 254).  Both
+// forms are computed and selected, branch-free; kA/kB are the broadcast bytes
+// 128 - m and 256 - m, lowm = (m <= 128).
+__device__ __forceinline__ uint32_t ge_u8(uint32_t a, uint32_t kA, uint32_t kB, bool lowm) {
+  const uint32_t lo = a & 0x7F7F7F7Fu;
+  const uint32_t rA = a | (lo + kA);
+  const uint32_t rB = a & (lo + kB);
+  return (lowm ? rA : rB) & 0x80808080u;
+}
+
+// u8 stage epilogue: scan + zero the wave's quarter.  One iteration covers 1024
+// targets (64 lanes x 16), which is exactly one threshold segment, so the
+// threshold m is wave-uniform.  A block passes a cheap prefilter when some byte
+// has a bit at or above the highest power of two <= m; only then are its targets
+// compared exactly (SWAR) and the flagged ones appended to the wave's queue
+// lane-parallel (one round per candidate of the busiest lane).
+template <int KPL>
+__device__ __forceinline__ void epilogue_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top,
+                                            CandQ& Q, const Stage& S, int wave, int lane,
+                                            int nbuf, int seg_shift, int64_t x_lab, int64_t gx,
+                                            double tau_sh, int mseg) {
+  const int qd = nbuf / kNW;
+  const int end = (wave + 1) * qd;
+  const int64_t tile_base = S.t << p.shift;
+  const bool score = (p.ablate & 2) == 0;
+  const int64_t xr64 = x_lab - tile_base;
+  const int xrel = (xr64 >= 0 && xr64 < (int64_t(1) << p.shift)) ? static_cast<int>(xr64) : -64;
+  for (int b0 = wave * qd; b0 < end; b0 += kWave * 4) {
+    const int b = b0 + lane * 4;
+    uint4 a = make_uint4(0, 0, 0, 0);
+    if (b < end) {
+      a = *reinterpret_cast<const uint4*>(acc + b);
+      *reinterpret_cast<uint4*>(acc + b) = make_uint4(0, 0, 0, 0);
+    }
+    const uint32_t m = static_cast<uint32_t>(readlane(mseg, (b0 << 2) >> seg_shift));
+    if (m > 255u || !score) continue;                          // no u8 count reaches m
+    const uint32_t pm = (0x100u - (0x80000000u >> __builtin_clz(m))) * 0x01010101u;
+    const uint32_t any = (a.x | a.y | a.z | a.w) & pm;
+    if (!ballot(any != 0)) continue;
+    const uint32_t kA = __builtin_amdgcn_perm(0u, 128u - m, 0u);   // byte 0 broadcast
+    const uint32_t kB = __builtin_amdgcn_perm(0u, 256u - m, 0u);
+    const bool lowm = m <= 128u;
+    // target (4*dw + byte) of the block -> bit 8*byte + 7 - dw
+    uint32_t F = ge_u8(a.x, kA, kB, lowm) | (ge_u8(a.y, kA, kB, lowm) >> 1) |
+                 (ge_u8(a.z, kA, kB, lowm) >> 2) | (ge_u8(a.w, kA, kB, lowm) >> 3);
+    const int i0 = b << 2;                                     // first target of the block
+    const int rel = xrel - i0;                                 // the source itself never counts
+    if (rel >= 0 && rel < 16) F &= ~(1u << ((rel & 3) * 8 + 7 - (rel >> 2)));
+    if (!ballot(F != 0)) continue;
+    wave_lds_fence();
+    for (;;) {
+      const bool has = F != 0;
+      const uint64_t mk = ballot(has);
+      if (!mk) break;
+      if (has) {
+        const int bit = __builtin_ctz(F);
+        F &= F - 1;
+        const int byte = bit >> 3, dw = 7 - (bit & 7);
+        const uint32_t w01 = (dw & 1) ? a.y : a.x;
+        const uint32_t w23 = (dw & 1) ? a.w : a.z;
+        const uint32_t wv = (dw & 2) ? w23 : w01;
+        const int pos = Q.n + mbcnt(mk);
+        Q.lab[pos] = static_cast<int>(tile_base + i0 + dw * 4 + byte);
+        Q.m[pos] = static_cast<int>((wv >> (byte * 8)) & 0xFFu);
+      }
+      Q.n += __popcll(mk);
+      if (Q.n >= kWave) flush<KPL>(p, Q, top, kWave, gx, tau_sh, lane);
+    }
+  }
+}
+
 // Scan + zero this wave's quarter of the stage's accumulator; queue the
 // targets whose M reaches their segment's threshold.
+// This lane's segment threshold for stage S: targets of segment `lane` need
+// M >= mseg to possibly reach the larger of tau_sh and the wave's k-th score.
 template <int KPL>
-__device__ __forceinline__ void epilogue(const CctParams& p, uint32_t* acc, TopK<KPL>& top,
-                                         CandQ& Q, const Stage& S, int wave, int lane, int nbuf,
-                                         int seg_shift, int64_t x_lab, int64_t gx,
-                                         double tau_sh) {
+__device__ __forceinline__ int stage_mseg(const TopK<KPL>& top, const Stage& S, int64_t gx,
+                                          double tau_sh) {
   double tau_w = tau_sh;
   if (top.full() && top.kth_s > tau_w) tau_w = top.kth_s;
   int mseg = 1;
   if (tau_w > 0.0) {
-    const int mn = compute_mneed(tau_w, gx + S.gq);
+    const int mn = mneed_lo(tau_w, gx + S.gq);
     mseg = mn > 1 ? mn : 1;
+  }
+  return mseg;
+}
+
+template <int KPL>
+__device__ __forceinline__ void epilogue(const CctParams& p, uint32_t* acc, TopK<KPL>& top,
+                                         CandQ& Q, const Stage& S, int wave, int lane, int nbuf,
+                                         int seg_shift, int64_t x_lab, int64_t gx,
+                                         double tau_sh, int mseg) {
+  if (S.lnp == 0) {
+    epilogue_u8<KPL>(p, acc, top, Q, S, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh, mseg);
+    return;
   }
   const int qd = nbuf / kNW;
   const int end = (wave + 1) * qd;
@@ -379,7 +527,7 @@ __device__ __forceinline__ void epilogue(const CctParams& p, uint32_t* acc, TopK
       *reinterpret_cast<uint4*>(acc + b) = make_uint4(0, 0, 0, 0);
     }
     const int i0 = pass_base + (b << tpd_shift);            // first target of the block
-    const int ms = __shfl(mseg, (i0 >> seg_shift) & (kSegs - 1), kWave);
+    const int ms = __shfl(mseg, (i0 >> seg_shift) & (kWave - 1), kWave);
     const uint32_t m = static_cast<uint32_t>(ms);
     const bool any = block_any(a, m, lnp);
     if (!score || !ballot(any)) continue;
@@ -404,31 +552,37 @@ __device__ __forceinline__ void epilogue(const CctParams& p, uint32_t* acc, TopK
   }
 }
 
-// Bounds of the row's venues for tiles tw and tw+1 (lane j = venue j, d <= 64).
+// Bounds of the row's venues for tile tw (lane j = venue j, d <= 64): bucket
+// (v_j, tw) is tile_ent[lo, hi), its largest C is mx.
 struct Window {
   int64_t tw;
   int v, c;
-  uint32_t lo, hi, mx, hi1, mx1;
+  uint32_t lo, hi, mx;
 };
 
-// Advance to the next tile that may hold a top-k target (d <= 64 rows).
+// Advance to the next tile that may hold a top-k target (d <= 64 rows).  The
+// window's loads for the following tile are issued as soon as the current
+// tile's values are consumed, so on a taken stage they complete behind the
+// scatter and epilogue.
 __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d, int lane,
                                            int64_t gx, double tau_sh, int seg_shift,
                                            bool no_scatter, Stage& S) {
   while (w.tw < p.T) {
     const int64_t t = w.tw++;
-    const uint32_t lo = w.lo, hi = w.hi, mx = w.mx;
-    w.lo = w.hi;
-    w.hi = w.hi1;
-    w.mx = w.mx1;
-    if (lane < d && t + 2 < p.T) {
-      const int64_t vb = static_cast<int64_t>(w.v) * p.T + t + 2;
-      w.hi1 = p.tile_off[vb + 1];
-      w.mx1 = p.tile_maxc[vb];
+    const uint32_t lo = w.lo, hi = w.hi;
+    // UB = sum_v C[x,v] * maxc[v,t] in 32 bits: a lane product of 2^25 or more
+    // (or such a total) means "unbounded" -- no skip, 32-bit passes
+    const uint64_t prod = static_cast<uint64_t>(static_cast<uint32_t>(w.c)) * w.mx;
+    const uint32_t ub32 = wave_sum_u32(prod > (1u << 25) ? (1u << 25) : static_cast<uint32_t>(prod));
+    int64_t ub = ub32 >= (1u << 25) ? (int64_t(1) << 40) : static_cast<int64_t>(ub32);
+    w.lo = hi;
+    if (lane < d && t + 1 < p.T) {
+      const int64_t vb = static_cast<int64_t>(w.v) * p.T + t + 1;
+      w.hi = p.tile_off[vb + 1];
+      w.mx = p.tile_maxc[vb];
     }
-    int64_t ub = wave_sum(static_cast<int64_t>(w.c) * mx);
     if (!p.use_bounds) ub = int64_t(1) << 40;
-    const bool take = ub > 0 && (tau_sh <= 0.0 || ub >= compute_mneed(tau_sh, gx + p.tile_gmin[t]));
+    const bool take = ub > 0 && (tau_sh <= 0.0 || ub >= mneed_lo(tau_sh, gx + p.tile_gmin[t]));
     if ((p.ablate & 8) && threadIdx.x == 0) {   // counters: tiles visited, tiles scanned
       atomicAdd(p.counter + 4, 1ull);
       if (take) atomicAdd(p.counter + 5, 1ull);
@@ -437,26 +591,37 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
     S.t = t;
     S.lnp = ub <= 0xFF ? 0 : ub <= 0xFFFF ? 1 : 2;
     S.pass = 0;
+    S.jc = 0;
     grp_set(S.G, lo, hi, w.c, d);
-    S.nb = no_scatter ? 0 : (S.G.nq + kTB * kU - 1) / (kTB * kU);
+    if (no_scatter) S.G.nq = 0;
+    S.nb = (S.G.nq + kTB * kU - 1) / (kTB * kU);
     S.gq = p.g_t[min((t << p.shift) + (static_cast<int64_t>(lane) << seg_shift),
                      p.n_targets - 1)];
     return true;
   }
+  S.G.base = 0; S.G.c = 0; S.G.pre = 0; S.G.nq = 0; S.G.nv = 1;   // no stage: dead loads only
+  S.nb = 0;
+  S.jc = 0;
   return false;
 }
 
 template <int KPL>
-__global__ __launch_bounds__(kTB) void k_cct_topk(CctParams p, int acc_dw) {
+__global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_cct_topk(CctParams p, int acc_dw) {
+  // All LDS is dynamic, so the accumulators start at LDS address 0 and each
+  // stage buffer is W-byte aligned (scatter_u8 ORs the in-tile offset in).
+  // Layout: [2 stage buffers | per-wave queues | tau_s | fill_s | row_s].
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ double tau_s[2][kNW];
-  __shared__ int fill_s[kNW];
-  __shared__ long long row_s;
+  double (*tau_s)[kNW] = reinterpret_cast<double (*)[kNW]>(lds + acc_dw + kNW * 2 * kQ);
+  int* fill_s = reinterpret_cast<int*>(lds + acc_dw + kNW * 2 * kQ + 4 * kNW);
+  long long& row_s = *reinterpret_cast<long long*>(lds + acc_dw + kNW * 2 * kQ + 5 * kNW);
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_u32*)lds));
+  const uint32_t lab_mask = ((1u << p.shift) - 1u) & ~3u;
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wave = tid / kWave;
   const int nbuf = 1 << (p.shift - 2);        // accumulator dwords per stage buffer
-  const int seg_shift = p.shift - 6;          // W / kSegs targets per threshold segment
+  // threshold segments of min(1024, W/4) targets: one epilogue iteration each
+  const int seg_shift = p.shift - 2 < 10 ? p.shift - 2 : 10;
   const bool no_add = (p.ablate & 1) != 0;
   const bool no_scatter = (p.ablate & 4) != 0;
   CandQ Q;
@@ -487,7 +652,7 @@ __global__ __launch_bounds__(kTB) void k_cct_topk(CctParams p, int acc_dw) {
       Window w;
       w.tw = 0;
       w.v = 0; w.c = 0;
-      w.lo = w.hi = w.mx = w.hi1 = w.mx1 = 0;
+      w.lo = w.hi = w.mx = 0;
       if (lane < d) {
         w.v = p.c_col[pb + lane];
         w.c = p.c_val[pb + lane];
@@ -495,33 +660,71 @@ __global__ __launch_bounds__(kTB) void k_cct_topk(CctParams p, int acc_dw) {
         w.lo = p.tile_off[vb];
         w.hi = p.tile_off[vb + 1];
         w.mx = p.tile_maxc[vb];
-        if (p.T > 1) { w.hi1 = p.tile_off[vb + 2]; w.mx1 = p.tile_maxc[vb + 1]; }
       }
       Stage cur;
       bool have = find_stage(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, cur);
+      // Batch 0 of the current stage is loaded one epilogue ahead.  It is issued
+      // unconditionally (a missing stage loads dead chunks with C = 0) so B has
+      // one definition in the loop and the register allocator need not copy it
+      // -- a copy would wait on the loads at once and expose their latency.
+      Batch B;
+      if (!have) cur.G.nq = 0;
+      issue(cur, 0, p.tile_ent, wave, lane, B, no_add);
+      // profiling aid (DPATHSIM_ABLATE & 16): shader-clock cycles per phase
+      const bool prof = (p.ablate & 16) != 0;
+      uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pc[7] = {0, 0, 0, 0, 0, 0, 0};
       while (have) {
-        uint32_t* acc = lds + (n & 1) * nbuf;
-        for (int b = 0; b < cur.nb; ++b) {
-          Batch B;
-          issue(cur, b, p.tile_ent, wave, lane, B, no_add);
-          scatter(B, cur, acc, p.shift);
+        if (prof) ts[0] = __builtin_amdgcn_s_memtime();
+        const int bi = p.dbuf ? (n & 1) : 0;
+        uint32_t* acc = lds + bi * nbuf;
+        const uint32_t buf = lds0 + static_cast<uint32_t>(bi * nbuf) * 4u;
+        scatter_any(B, cur, acc, buf, lab_mask, p.shift);
+        for (int b = 1; b < cur.nb; ++b) {
+          Batch B2;
+          issue(cur, b, p.tile_ent, wave, lane, B2, no_add);
+          scatter_any(B2, cur, acc, buf, lab_mask, p.shift);
         }
-        __syncthreads();
-        if (n >= 1) {
-          double tm = tau_s[(n - 1) & 1][0];
-#pragma unroll
-          for (int i = 1; i < kNW; ++i) tm = tau_s[(n - 1) & 1][i] > tm ? tau_s[(n - 1) & 1][i] : tm;
-          tau_sh = tm;
-        }
-        epilogue<KPL>(p, acc, top, Q, cur, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh);
-        // stage end: score what is queued while the wave's list is filling or
-        // the queue is half full; otherwise let it ride (one round trip per 64)
+        if (prof) ts[1] = __builtin_amdgcn_s_memtime();
+        // score what is queued while the wave's list is filling or the queue is
+        // half full (one memory round trip per 64 candidates); done here, while
+        // no prefetch is in flight, so its loads do not wait on the prefetch
         if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
           flush<KPL>(p, Q, top, Q.n, gx, tau_sh, lane);
         if (lane == 0) tau_s[n & 1][wave] = top.full() ? top.kth_s : -1.0;
+        if (prof) ts[2] = __builtin_amdgcn_s_memtime();
+        __syncthreads();
+        if (prof) ts[3] = __builtin_amdgcn_s_memtime();
+        double tm = tau_s[n & 1][0];
+#pragma unroll
+        for (int i = 1; i < kNW; ++i) tm = tau_s[n & 1][i] > tm ? tau_s[n & 1][i] : tm;
+        tau_sh = tm;
+        const int mseg = stage_mseg(top, cur, gx, tau_sh);
+        // find the next stage and put its first loads in flight before this
+        // stage's epilogue (pure LDS work unless the queue fills up)
+        Stage nxt;
+        bool have_n;
+        if (cur.pass + 1 < (1 << cur.lnp)) { nxt = cur; ++nxt.pass; nxt.jc = 0; have_n = true; }
+        else have_n = find_stage(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, nxt);
+        if (!have_n) nxt.G.nq = 0;
+        if (prof) ts[4] = __builtin_amdgcn_s_memtime();
+        issue(nxt, 0, p.tile_ent, wave, lane, B, no_add);
+        if (prof) ts[5] = __builtin_amdgcn_s_memtime();
+        epilogue<KPL>(p, acc, top, Q, cur, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh, mseg);
+        if (prof) ts[6] = __builtin_amdgcn_s_memtime();
+        if (!p.dbuf) __syncthreads();   // one buffer: every wave has zeroed its quarter
+        if (prof) {
+          ts[7] = __builtin_amdgcn_s_memtime();
+#pragma unroll
+          for (int i = 0; i < 7; ++i) pc[i] += ts[i + 1] - ts[i];
+        }
         ++n;
-        if (cur.pass + 1 < (1 << cur.lnp)) ++cur.pass;
-        else have = find_stage(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, cur);
+        cur = nxt;
+        have = have_n;
+      }
+      if (prof && lane == 0) {   // scatter, flush, barrier 1, find, prefetch, epilogue, barrier 2
+#pragma unroll
+        for (int i = 0; i < 7; ++i) atomicAdd(p.counter + 8 + i, static_cast<unsigned long long>(pc[i]));
+        atomicAdd(p.counter + 15, static_cast<unsigned long long>(n));
       }
     } else if (d > kWave) {
       // ---- rows with more than 64 venues: the same stages, synchronously
@@ -536,14 +739,16 @@ __global__ __launch_bounds__(kTB) void k_cct_topk(CctParams p, int acc_dw) {
         ub = wave_sum(ub);
         if (!p.use_bounds) ub = int64_t(1) << 40;
         if (ub == 0) continue;
-        if (tau_sh > 0.0 && ub < compute_mneed(tau_sh, gx + p.tile_gmin[t])) continue;
+        if (tau_sh > 0.0 && ub < mneed_lo(tau_sh, gx + p.tile_gmin[t])) continue;
         Stage S;
         S.t = t;
         S.lnp = ub <= 0xFF ? 0 : ub <= 0xFFFF ? 1 : 2;
         S.gq = p.g_t[min((t << p.shift) + (static_cast<int64_t>(lane) << seg_shift),
                          p.n_targets - 1)];
         for (S.pass = 0; S.pass < (1 << S.lnp); ++S.pass) {
-          uint32_t* acc = lds + (n & 1) * nbuf;
+          const int bi = p.dbuf ? (n & 1) : 0;
+          uint32_t* acc = lds + bi * nbuf;
+          const uint32_t buf = lds0 + static_cast<uint32_t>(bi * nbuf) * 4u;
           for (int g0 = 0; !no_scatter && g0 < d; g0 += kWave) {
             const int j = g0 + lane;
             uint32_t lo = 0, hi = 0;
@@ -555,24 +760,25 @@ __global__ __launch_bounds__(kTB) void k_cct_topk(CctParams p, int acc_dw) {
               c = p.c_val[pb + j];
             }
             grp_set(S.G, lo, hi, c, d - g0 < kWave ? d - g0 : kWave);
+            S.jc = 0;
             S.nb = (S.G.nq + kTB * kU - 1) / (kTB * kU);
             for (int b = 0; b < S.nb; ++b) {
               Batch B;
               issue(S, b, p.tile_ent, wave, lane, B, no_add);
-              scatter(B, S, acc, p.shift);
+              scatter_any(B, S, acc, buf, lab_mask, p.shift);
             }
           }
-          __syncthreads();
-          if (n >= 1) {
-            double tm = tau_s[(n - 1) & 1][0];
-#pragma unroll
-            for (int i = 1; i < kNW; ++i) tm = tau_s[(n - 1) & 1][i] > tm ? tau_s[(n - 1) & 1][i] : tm;
-            tau_sh = tm;
-          }
-          epilogue<KPL>(p, acc, top, Q, S, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh);
           if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
             flush<KPL>(p, Q, top, Q.n, gx, tau_sh, lane);
           if (lane == 0) tau_s[n & 1][wave] = top.full() ? top.kth_s : -1.0;
+          __syncthreads();
+          double tm = tau_s[n & 1][0];
+#pragma unroll
+          for (int i = 1; i < kNW; ++i) tm = tau_s[n & 1][i] > tm ? tau_s[n & 1][i] : tm;
+          tau_sh = tm;
+          epilogue<KPL>(p, acc, top, Q, S, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh,
+                        stage_mseg(top, S, gx, tau_sh));
+          if (!p.dbuf) __syncthreads();
           ++n;
         }
       }
@@ -654,10 +860,12 @@ int log2_exact(int32_t w) {
 
 template <int KPL>
 int launch(const CctParams& p, hipStream_t st) {
-  // two stage buffers of W/4 dwords; the row-end merge reuses them (16 B per entry)
-  int acc_dw = 2 * (1 << (p.shift - 2));
+  // one or two stage buffers of W/4 dwords; the row-end merge reuses them (16 B
+  // per entry)
+  int acc_dw = (p.dbuf ? 2 : 1) * (1 << (p.shift - 2));
   if (acc_dw < 4 * kNW * p.k) acc_dw = 4 * kNW * p.k;
-  const size_t lds = (static_cast<size_t>(acc_dw) + kNW * 2 * kQ) * sizeof(uint32_t);
+  // + tau_s (2*kNW doubles) + fill_s (kNW ints) + row_s (one 8-byte slot)
+  const size_t lds = (static_cast<size_t>(acc_dw) + kNW * 2 * kQ + 5 * kNW + 2) * sizeof(uint32_t);
   DPS_HIP_RET(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cct_topk<KPL>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   static_cast<int>(lds)));
@@ -692,8 +900,8 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
                  size_t ws_bytes, void* stream) {
   (void)n_mids;
   const int shift = log2_exact(tile_w);
-  DPS_REQUIRE(shift >= 8 && shift <= 14, DPS_ERR_UNSUPPORTED,
-              "tile_w must be a power of two in [256, 16384], got %d", tile_w);
+  DPS_REQUIRE(shift >= 8 && shift <= 15, DPS_ERR_UNSUPPORTED,
+              "tile_w must be a power of two in [256, 32768], got %d", tile_w);
   DPS_REQUIRE(k >= 1 && k <= 256, DPS_ERR_UNSUPPORTED, "k must be in [1, 256], got %d", k);
   DPS_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= n_targets, DPS_ERR_INVALID,
               "row range [%lld, %lld) outside [0, %lld)", static_cast<long long>(row_begin),
@@ -716,12 +924,13 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   p.n_targets = n_targets;
   p.T = (n_targets + tile_w - 1) / tile_w;
   p.shift = shift;
+  p.dbuf = shift <= 14;   // 2 x W bytes of u8 accumulators up to W = 16384, one 32 KB buffer above
   p.row_begin = row_begin; p.n_rows = n_rows; p.k = k;
   p.out_idx = out_idx; p.out_cnt = out_cnt; p.out_score = out_score;
   p.counter = static_cast<unsigned long long*>(ws);
   p.ablate = 0;
   if (const char* ab = std::getenv("DPATHSIM_ABLATE")) p.ablate = std::atoi(ab);
-  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 8) ? 64 : sizeof(unsigned long long), st));
+  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : sizeof(unsigned long long), st));
   if (k <= 64) return launch<1>(p, st);
   if (k <= 128) return launch<2>(p, st);
   return launch<4>(p, st);

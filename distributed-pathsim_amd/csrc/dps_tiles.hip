@@ -69,10 +69,15 @@ __global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, i
 
 __global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__ off,
                                                      const uint32_t* __restrict__ cursor,
-                                                     int64_t n, uint32_t* __restrict__ ent) {
+                                                     int64_t n, uint32_t lab_mask,
+                                                     uint32_t* __restrict__ ent) {
+  // Padding entries have C = 0 (they add nothing) and a label that walks over
+  // the tile's dwords, so the hot kernel's branch-free u8 adds of padding do not
+  // pile onto one LDS bank.
   for (int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; b < n;
        b += static_cast<int64_t>(gridDim.x) * kBlock)
-    for (int64_t i = off[b] + cursor[b]; i < off[b + 1]; ++i) ent[i] = 0u;
+    for (int64_t i = off[b] + cursor[b]; i < off[b + 1]; ++i)
+      ent[i] = (static_cast<uint32_t>(i) << 2) & lab_mask;
 }
 
 __global__ __launch_bounds__(kBlock) void k_tile_off32(const int64_t* __restrict__ p64,
@@ -237,8 +242,8 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
                        int64_t* tile_gmin, int32_t* status_dev, void* ws, size_t ws_bytes,
                        void* stream) {
   const int shift = log2_exact(tile_w);
-  DPS_REQUIRE(shift >= 8 && shift <= 14, DPS_ERR_UNSUPPORTED,
-              "tile_w must be a power of two in [256, 16384], got %d", tile_w);
+  DPS_REQUIRE(shift >= 8 && shift <= 15, DPS_ERR_UNSUPPORTED,
+              "tile_w must be a power of two in [256, 32768], got %d", tile_w);
   DPS_REQUIRE(n_targets >= 0 && n_mids >= 0, DPS_ERR_INVALID, "negative size");
   DPS_REQUIRE(n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "n_targets exceeds int32");
   DPS_REQUIRE(!tile_gmin || g, DPS_ERR_INVALID, "tile_gmin needs g");
@@ -280,7 +285,8 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     DPS_LAUNCHED();
   }
   if (nb > 0) {
-    k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(off64, cursor, nb, tile_ent);
+    k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(
+        off64, cursor, nb, ((static_cast<uint32_t>(tile_w) - 1u) & ~3u), tile_ent);
     DPS_LAUNCHED();
   }
   return DPS_OK;
@@ -292,7 +298,7 @@ int dps_walk_row(const int32_t* src_col, const int32_t* src_val, int64_t src_len
                  void* stream) {
   (void)n_mids;
   const int shift = log2_exact(tile_w);
-  DPS_REQUIRE(shift >= 8 && shift <= 14, DPS_ERR_UNSUPPORTED, "bad tile_w %d", tile_w);
+  DPS_REQUIRE(shift >= 8 && shift <= 15, DPS_ERR_UNSUPPORTED, "bad tile_w %d", tile_w);
   DPS_REQUIRE(src_len >= 0 && n_targets >= 0, DPS_ERR_INVALID, "negative size");
   auto st = static_cast<hipStream_t>(stream);
   const int64_t T = (n_targets + tile_w - 1) / tile_w;

@@ -16,7 +16,7 @@ import torch
 from . import _lib
 from .graph import TypedTables
 
-DEFAULT_TILE_W = 16384
+DEFAULT_TILE_W = 32768
 
 
 def _ptr(t):
@@ -50,8 +50,8 @@ class PathSimEngine:
         _lib.load()
         self.typed = typed
         self.device = torch.device(device if device is not None else "cuda")
-        if tile_w & (tile_w - 1) or not 256 <= tile_w <= 16384:
-            raise ValueError("tile_w must be a power of two in [256, 16384]")
+        if tile_w & (tile_w - 1) or not 256 <= tile_w <= 32768:
+            raise ValueError("tile_w must be a power of two in [256, 32768]")
         self.tile_w = int(tile_w)
         self.tile_skip = True
         self.info = BuildInfo()

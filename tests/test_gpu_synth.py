@@ -23,7 +23,7 @@ def _check(eng, co, k, rows=None):
                            f"orc {oi[bad[0]]} {oc[bad[0]]} {os_[bad[0]]}")
 
 
-@pytest.mark.parametrize("tile_w", [256, 1024, 4096])
+@pytest.mark.parametrize("tile_w", [256, 1024, 4096, 32768])
 def test_synth_20k_top10(tile_w):
     from dpathsim.engine import build_engine
     from dpathsim.synth import synth_dblp
@@ -70,13 +70,14 @@ def test_aptpa_multi_topic():
     _check(build_engine(t, tile_w=1024), _oracle(t), 10)
 
 
-def test_config3_sample_rows():
-    """Full-size config3 (1M authors): a 3000-row slice vs the C oracle."""
+@pytest.mark.parametrize("tile_w", [16384, 32768])
+def test_config3_sample_rows(tile_w):
+    """Full-size config3 (1M authors): two 1500-row slices vs the C oracle."""
     from dpathsim.engine import build_engine
     from dpathsim.synth import synth_config
     g = synth_config("config3")
     t = g.typed()
-    eng = build_engine(t)
+    eng = build_engine(t, tile_w=tile_w)
     co = _oracle(t)
     _check(eng, co, 10, rows=(0, 1500))
     _check(eng, co, 10, rows=(777_000, 778_500))
