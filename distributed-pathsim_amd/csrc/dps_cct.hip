@@ -39,6 +39,15 @@
 namespace dps {
 namespace {
 
+// Profiling aids (DPATHSIM_ABLATE=8 event counters, =16 shader-clock phase
+// timers) are compiled in only with -DDPS_PROFILE; the production build keeps
+// their state out of the register budget.
+#ifdef DPS_PROFILE
+constexpr bool kProfile = true;
+#else
+constexpr bool kProfile = false;
+#endif
+
 constexpr int kTB = 256;            // threads per workgroup
 constexpr int kNW = kTB / kWave;    // waves per workgroup
 constexpr int kU = 4;               // 16-B chunk loads in flight per lane
@@ -51,19 +60,19 @@ __device__ __forceinline__ bool better(double s1, int y1, double s2, int y2) {
   return s1 > s2 || (s1 == s2 && y1 < y2);
 }
 
-// Integer threshold, conservative: a lower bound on the smallest m >= 0 with
-// fl(2m / den) >= kth.  Every target y with g[y] >= g0 has gx + g[y] >= den :=
-// gx + g0, so (rounding is monotone) fl(2M/(gx+g[y])) <= fl(2M/den), and
-// m -> fl(2m/den) is nondecreasing: a target with M below the exact threshold
-// m* scores strictly below kth and cannot enter the top-k, ties included.
-// fl(2m*/den) >= kth gives m* >= kth*den/2*(1 - 2^-53); the value below is
-// at most kth*den/2*(1 - 2^-50)*(1 + 2^-52) < that, so it never exceeds m*
-// (it is m* or m* - 1 in practice).  Two multiplies, no division.
+// Integer threshold: a lower bound on m* = the smallest m >= 0 with
+// fl(2m / den) >= kth, equal to m* in practice.  Every target y with g[y] >= g0
+// has gx + g[y] >= den := gx + g0, so (rounding is monotone) fl(2M/(gx+g[y])) <=
+// fl(2M/den), and m -> fl(2m/den) is nondecreasing: a target with M < m* scores
+// strictly below kth and cannot enter the top-k, ties included.
+// fl(2m*/den) >= kth gives 2m*/den >= kth*(1 - 2^-53), i.e. m* >= r*(1 - 2^-53)
+// with r = kth*den/2; the computed r' = kth*den*0.5*(1 - 2^-50) (two roundings)
+// is below r*(1 - 2^-53), so ceil(r') <= m*.  Two multiplies, no division.
 __device__ __forceinline__ int mneed_lo(double kth, int64_t den) {
   if (kth <= 0.0 || den <= 0) return 0;
   const double r = kth * static_cast<double>(den) * (0.5 * (1.0 - 0x1p-50));
   if (r >= 2147483000.0) return INT32_MAX;
-  return static_cast<int>(r);   // truncation = floor for r >= 0
+  return static_cast<int>(ceil(r));
 }
 
 // Register-resident sorted top-k of one wave: rank r*64 + lane in slot r.
@@ -240,7 +249,8 @@ struct Batch {
 // venue boundaries resolves each lane's venue with chunk_venue().  Loads past
 // the stage's last chunk are skipped (uniform) and marked dead (c = 0).
 __device__ __forceinline__ void issue(Stage& S, int b, const uint32_t* __restrict__ ent,
-                                      int wave, int lane, Batch& B, bool no_add) {
+                                      int wave, int lane, Batch& B, bool no_add,
+                                      int p_ablate = 0, unsigned long long* p_counter = nullptr) {
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const int q0 = b * (kTB * kU) + u * kTB + wave * kWave;   // wave-uniform
@@ -256,6 +266,7 @@ __device__ __forceinline__ void issue(Stage& S, int b, const uint32_t* __restric
     const bool live = q < S.G.nq;
     uint32_t bj;
     int cj;
+    if ((kProfile && (p_ablate & 8)) && lane == 0) atomicAdd(p_counter + (q0 + kWave - 1 < jn ? 20 : 21), 1ull);
     if (q0 + kWave - 1 < jn) {
       bj = readlane(S.G.base, S.jc);
       cj = readlane(S.G.c, S.jc);
@@ -378,7 +389,7 @@ __device__ __forceinline__ void flush(const CctParams& p, CandQ& Q, TopK<KPL>& t
   if (mv) { Q.lab[lane] = tl; Q.m[lane] = tm; }
   Q.n -= n;
   uint64_t mask = ballot(cand);
-  if ((p.ablate & 8) && lane == 0) {       // counters: flushes, candidates, passers
+  if ((kProfile && (p.ablate & 8)) && lane == 0) {       // counters: flushes, candidates, passers
     atomicAdd(p.counter + 1, 1ull);
     atomicAdd(p.counter + 2, static_cast<unsigned long long>(n));
     atomicAdd(p.counter + 3, static_cast<unsigned long long>(__popcll(mask)));
@@ -422,7 +433,6 @@ __device__ __forceinline__ uint32_t ge_u8(uint32_t a, uint32_t kA, uint32_t kB, 
   const uint32_t rB = a & (lo + kB);
   return (lowm ? rA : rB) & 0x80808080u;
 }
-
 // u8 stage epilogue: scan + zero the wave's quarter.  One iteration covers 1024
 // targets (64 lanes x 16), which is exactly one threshold segment, so the
 // threshold m is wave-uniform.  A block passes a cheap prefilter when some byte
@@ -451,7 +461,9 @@ __device__ __forceinline__ void epilogue_u8(const CctParams& p, uint32_t* acc, T
     if (m > 255u || !score) continue;                          // no u8 count reaches m
     const uint32_t pm = (0x100u - (0x80000000u >> __builtin_clz(m))) * 0x01010101u;
     const uint32_t any = (a.x | a.y | a.z | a.w) & pm;
+    if ((kProfile && (p.ablate & 8)) && lane == 0) atomicAdd(p.counter + 16, 1ull);   // iterations scanned
     if (!ballot(any != 0)) continue;
+    if ((kProfile && (p.ablate & 8)) && lane == 0) atomicAdd(p.counter + 17, 1ull);   // prefilter passes
     const uint32_t kA = __builtin_amdgcn_perm(0u, 128u - m, 0u);   // byte 0 broadcast
     const uint32_t kB = __builtin_amdgcn_perm(0u, 256u - m, 0u);
     const bool lowm = m <= 128u;
@@ -462,11 +474,13 @@ __device__ __forceinline__ void epilogue_u8(const CctParams& p, uint32_t* acc, T
     const int rel = xrel - i0;                                 // the source itself never counts
     if (rel >= 0 && rel < 16) F &= ~(1u << ((rel & 3) * 8 + 7 - (rel >> 2)));
     if (!ballot(F != 0)) continue;
+    if ((kProfile && (p.ablate & 8)) && lane == 0) atomicAdd(p.counter + 18, 1ull);   // exact passes
     wave_lds_fence();
     for (;;) {
       const bool has = F != 0;
       const uint64_t mk = ballot(has);
       if (!mk) break;
+      if ((kProfile && (p.ablate & 8)) && lane == 0) atomicAdd(p.counter + 19, 1ull); // extraction rounds
       if (has) {
         const int bit = __builtin_ctz(F);
         F &= F - 1;
@@ -583,7 +597,7 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
     }
     if (!p.use_bounds) ub = int64_t(1) << 40;
     const bool take = ub > 0 && (tau_sh <= 0.0 || ub >= mneed_lo(tau_sh, gx + p.tile_gmin[t]));
-    if ((p.ablate & 8) && threadIdx.x == 0) {   // counters: tiles visited, tiles scanned
+    if ((kProfile && (p.ablate & 8)) && threadIdx.x == 0) {   // counters: tiles visited, tiles scanned
       atomicAdd(p.counter + 4, 1ull);
       if (take) atomicAdd(p.counter + 5, 1ull);
     }
@@ -669,9 +683,9 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       // -- a copy would wait on the loads at once and expose their latency.
       Batch B;
       if (!have) cur.G.nq = 0;
-      issue(cur, 0, p.tile_ent, wave, lane, B, no_add);
+      issue(cur, 0, p.tile_ent, wave, lane, B, no_add, p.ablate, p.counter);
       // profiling aid (DPATHSIM_ABLATE & 16): shader-clock cycles per phase
-      const bool prof = (p.ablate & 16) != 0;
+      const bool prof = kProfile && (p.ablate & 16) != 0;
       uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pc[7] = {0, 0, 0, 0, 0, 0, 0};
       while (have) {
         if (prof) ts[0] = __builtin_amdgcn_s_memtime();
@@ -681,7 +695,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         scatter_any(B, cur, acc, buf, lab_mask, p.shift);
         for (int b = 1; b < cur.nb; ++b) {
           Batch B2;
-          issue(cur, b, p.tile_ent, wave, lane, B2, no_add);
+          issue(cur, b, p.tile_ent, wave, lane, B2, no_add, p.ablate, p.counter);
           scatter_any(B2, cur, acc, buf, lab_mask, p.shift);
         }
         if (prof) ts[1] = __builtin_amdgcn_s_memtime();
@@ -707,7 +721,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         else have_n = find_stage(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, nxt);
         if (!have_n) nxt.G.nq = 0;
         if (prof) ts[4] = __builtin_amdgcn_s_memtime();
-        issue(nxt, 0, p.tile_ent, wave, lane, B, no_add);
+        issue(nxt, 0, p.tile_ent, wave, lane, B, no_add, p.ablate, p.counter);
         if (prof) ts[5] = __builtin_amdgcn_s_memtime();
         epilogue<KPL>(p, acc, top, Q, cur, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh, mseg);
         if (prof) ts[6] = __builtin_amdgcn_s_memtime();

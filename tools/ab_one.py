@@ -12,7 +12,7 @@ from dpathsim.engine import build_engine
 R = int(os.environ.get("AB_ROWS", "1000000"))
 cfg = os.environ.get("AB_CONFIG", "config3")
 k = int(os.environ.get("AB_K", "10"))
-eng = build_engine(synth_config(cfg).typed(), tile_w=int(os.environ.get("AB_W", "16384")))
+eng = build_engine(synth_config(cfg).typed(), tile_w=int(os.environ.get("AB_W", "32768")))
 R = min(R, eng.typed.n_authors)
 eng.topk(k, 0, 20000); torch.cuda.synchronize()
 best = 1e30
