@@ -17,45 +17,65 @@ __device__ __forceinline__ int64_t bound_from(const int64_t* dev, int64_t host) 
 // ---------------------------------------------------------------------------
 // A2: typed incidence extraction (DPathSim_APVPA.py:78-84).  Wave-aggregated
 // atomic append: one atomic per wave per output list.
+constexpr int kExtractPer = 16;   // edges per lane per wave chunk
+
 __global__ __launch_bounds__(kBlock) void k_extract(
     const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
     const uint8_t* __restrict__ rel, int64_t n, const uint8_t* __restrict__ ntype,
     const int32_t* __restrict__ rowid, const int32_t* __restrict__ colid,
     int32_t* __restrict__ ap_r, int32_t* __restrict__ ap_c, unsigned long long* n_ap,
     int32_t* __restrict__ px_r, int32_t* __restrict__ px_c, unsigned long long* n_px) {
+  // A wave owns chunks of kExtractPer*64 consecutive edges: pass 1 classifies
+  // them (flags kept as bitmasks), one atomicAdd per output list reserves the
+  // chunk's slots, pass 2 writes the pairs in edge order within the chunk.
   const int lane = lane_id();
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  const int64_t n_round = (n + kWave - 1) / kWave * kWave;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n_round;
-       i += stride) {
-    bool is_ap = false, is_px = false;
-    int32_t s = 0, d = 0;
-    if (i < n) {
-      s = src[i];
-      d = dst[i];
-      const uint8_t r = rel[i];
-      const uint8_t td = ntype[d];
-      is_ap = (r == DPS_R_AP) && (td == DPS_T_PAPER);
-      is_px = (r == DPS_R_PX) && (ntype[s] == DPS_T_PAPER) && (td == DPS_T_MID);
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  constexpr int64_t kChunk = static_cast<int64_t>(kExtractPer) * kWave;
+  for (int64_t c0 = wave0 * kChunk; c0 < n; c0 += nwaves * kChunk) {
+    uint32_t f_ap = 0, f_px = 0;
+    int c_ap = 0, c_px = 0;
+#pragma unroll
+    for (int u = 0; u < kExtractPer; ++u) {
+      const int64_t i = c0 + u * kWave + lane;
+      bool is_ap = false, is_px = false;
+      if (i < n) {
+        const int32_t s = src[i], d = dst[i];
+        const uint8_t r = rel[i];
+        const uint8_t td = ntype[d];
+        is_ap = (r == DPS_R_AP) && (td == DPS_T_PAPER);
+        is_px = (r == DPS_R_PX) && (ntype[s] == DPS_T_PAPER) && (td == DPS_T_MID);
+      }
+      const uint64_t m_ap = ballot(is_ap), m_px = ballot(is_px);
+      f_ap |= is_ap ? (1u << u) : 0u;
+      f_px |= is_px ? (1u << u) : 0u;
+      c_ap += __popcll(m_ap);
+      c_px += __popcll(m_px);
     }
-    const uint64_t m_ap = ballot(is_ap);
-    const uint64_t m_px = ballot(is_px);
     unsigned long long b_ap = 0, b_px = 0;
     if (lane == 0) {
-      if (m_ap) b_ap = atomicAdd(n_ap, static_cast<unsigned long long>(__popcll(m_ap)));
-      if (m_px) b_px = atomicAdd(n_px, static_cast<unsigned long long>(__popcll(m_px)));
+      if (c_ap) b_ap = atomicAdd(n_ap, static_cast<unsigned long long>(c_ap));
+      if (c_px) b_px = atomicAdd(n_px, static_cast<unsigned long long>(c_px));
     }
-    b_ap = __shfl(b_ap, 0, kWave);
-    b_px = __shfl(b_px, 0, kWave);
-    if (is_ap) {
-      const int64_t o = static_cast<int64_t>(b_ap) + mbcnt(m_ap);
-      ap_r[o] = rowid[s];
-      ap_c[o] = colid[d];
-    }
-    if (is_px) {
-      const int64_t o = static_cast<int64_t>(b_px) + mbcnt(m_px);
-      px_r[o] = colid[s];
-      px_c[o] = colid[d];
+    int64_t o_ap = static_cast<int64_t>(__shfl(b_ap, 0, kWave));
+    int64_t o_px = static_cast<int64_t>(__shfl(b_px, 0, kWave));
+#pragma unroll
+    for (int u = 0; u < kExtractPer; ++u) {
+      const int64_t i = c0 + u * kWave + lane;
+      const bool is_ap = (f_ap >> u) & 1u, is_px = (f_px >> u) & 1u;
+      const uint64_t m_ap = ballot(is_ap), m_px = ballot(is_px);
+      if (is_ap) {
+        const int64_t o = o_ap + mbcnt(m_ap);
+        ap_r[o] = rowid[src[i]];
+        ap_c[o] = colid[dst[i]];
+      }
+      if (is_px) {
+        const int64_t o = o_px + mbcnt(m_px);
+        px_r[o] = colid[src[i]];
+        px_c[o] = colid[dst[i]];
+      }
+      o_ap += __popcll(m_ap);
+      o_px += __popcll(m_px);
     }
   }
 }
@@ -273,6 +293,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_len(const int64_t* __restrict
   const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  int64_t wave_total = 0;   // one atomic per wave, not per row
   for (int64_t i = wave0; i < n_out; i += nwaves) {
     const int64_t r = out_row_src(rows, i);
     const int64_t b = ap_ptr[r], e = ap_ptr[r + 1];
@@ -282,11 +303,11 @@ __global__ __launch_bounds__(kBlock) void k_expand_len(const int64_t* __restrict
       sum += px_ptr[p + 1] - px_ptr[p];
     }
     sum = wave_sum(sum);
-    if (lane == 0) {
-      if (e_len) e_len[i] = sum;
-      if (e_total) atomicAdd(e_total, static_cast<unsigned long long>(sum));
-    }
+    wave_total += sum;
+    if (lane == 0 && e_len) e_len[i] = sum;
   }
+  if (lane == 0 && e_total && wave_total)
+    atomicAdd(e_total, static_cast<unsigned long long>(wave_total));
 }
 
 __global__ __launch_bounds__(kBlock) void k_expand(const int64_t* __restrict__ ap_ptr,
@@ -331,18 +352,33 @@ __global__ __launch_bounds__(kBlock) void k_paper_indeg(const int64_t* __restric
     atomicAdd(&indeg[ap_col[j]], 1);
 }
 
+constexpr int64_t kMidLds = 6144;   // mids whose walk sums are reduced in LDS per block
+
 __global__ __launch_bounds__(kBlock) void k_mid_walks(const int64_t* __restrict__ px_ptr,
                                                       const int32_t* __restrict__ px_col,
-                                                      int64_t n_papers,
+                                                      int64_t n_papers, int64_t n_mids,
                                                       const int32_t* __restrict__ indeg,
                                                       unsigned long long* __restrict__ s) {
+  // per-block partial sums in LDS (hot venues would otherwise take one global
+  // atomic per paper), flushed with one atomic per mid and block
+  __shared__ unsigned long long s_lds[kMidLds];
+  const bool lds = n_mids <= kMidLds;
+  if (lds)
+    for (int64_t i = threadIdx.x; i < n_mids; i += kBlock) s_lds[i] = 0;
+  __syncthreads();
   for (int64_t p = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; p < n_papers;
        p += static_cast<int64_t>(gridDim.x) * kBlock) {
     const int d = indeg[p];
     if (d == 0) continue;
-    for (int64_t j = px_ptr[p]; j < px_ptr[p + 1]; ++j)
-      atomicAdd(&s[px_col[j]], static_cast<unsigned long long>(d));
+    for (int64_t j = px_ptr[p]; j < px_ptr[p + 1]; ++j) {
+      if (lds) atomicAdd(&s_lds[px_col[j]], static_cast<unsigned long long>(d));
+      else atomicAdd(&s[px_col[j]], static_cast<unsigned long long>(d));
+    }
   }
+  __syncthreads();
+  if (lds)
+    for (int64_t i = threadIdx.x; i < n_mids; i += kBlock)
+      if (s_lds[i]) atomicAdd(&s[i], s_lds[i]);
 }
 
 __global__ __launch_bounds__(kBlock) void k_global_walks(const int64_t* __restrict__ c_ptr,
@@ -430,7 +466,7 @@ int dps_extract_incidence(const int32_t* edge_src, const int32_t* edge_dst,
   DPS_REQUIRE(edge_src && edge_dst && edge_rel && node_type && node_rowid && node_colid &&
                   ap_row && ap_col && px_row && px_col,
               DPS_ERR_INVALID, "null array");
-  k_extract<<<grid_for(n_edges, kBlock), kBlock, 0, st>>>(
+  k_extract<<<grid_for((n_edges + kExtractPer - 1) / kExtractPer, kBlock), kBlock, 0, st>>>(
       edge_src, edge_dst, edge_rel, n_edges, node_type, node_rowid, node_colid, ap_row, ap_col,
       reinterpret_cast<unsigned long long*>(n_ap), px_row, px_col,
       reinterpret_cast<unsigned long long*>(n_px));
@@ -595,8 +631,8 @@ int dps_mid_walks(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_ap_row
   DPS_HIP_RET(hipMemsetAsync(paper_indeg_ws, 0, n_papers * sizeof(int32_t), st));
   k_paper_indeg<<<2048, kBlock, 0, st>>>(ap_ptr, ap_col, n_ap_rows, paper_indeg_ws);
   DPS_LAUNCHED();
-  k_mid_walks<<<grid_for(n_papers, kBlock), kBlock, 0, st>>>(
-      px_ptr, px_col, n_papers, paper_indeg_ws, reinterpret_cast<unsigned long long*>(s));
+  k_mid_walks<<<grid_for(n_papers, kBlock, 1024), kBlock, 0, st>>>(
+      px_ptr, px_col, n_papers, n_mids, paper_indeg_ws, reinterpret_cast<unsigned long long*>(s));
   DPS_LAUNCHED();
   return DPS_OK;
 }

@@ -33,6 +33,8 @@ __device__ __forceinline__ int64_t label_of(const int32_t* rank, int64_t y) {
   return rank ? static_cast<int64_t>(rank[y]) : y;
 }
 
+constexpr int64_t kTileGminLds = 4096;   // tiles whose g minimum is reduced in LDS
+
 __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict__ c_ptr,
                                                        const int32_t* __restrict__ c_col,
                                                        const int32_t* __restrict__ c_val,
@@ -43,12 +45,22 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
                                                        uint32_t* __restrict__ maxc,
                                                        unsigned long long* __restrict__ gmin,
                                                        int32_t* __restrict__ status) {
+  // per-block minimum g of each tile in LDS (one global atomicMin per tile and
+  // block instead of one per row onto T hot addresses) when T fits
+  __shared__ unsigned long long gmin_s[kTileGminLds];
+  const bool lds_gmin = gmin && T <= kTileGminLds;
+  if (lds_gmin)
+    for (int64_t i = threadIdx.x; i < T; i += kBlock) gmin_s[i] = ~0ull;
+  __syncthreads();
   const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
   for (int64_t y = wave0; y < n_rows; y += nwaves) {
     const int64_t t = label_of(rank, y) >> shift;
-    if (lane == 0 && gmin) atomicMin(&gmin[t], static_cast<unsigned long long>(g[y]));
+    if (lane == 0 && gmin) {
+      if (lds_gmin) atomicMin(&gmin_s[t], static_cast<unsigned long long>(g[y]));
+      else atomicMin(&gmin[t], static_cast<unsigned long long>(g[y]));
+    }
     for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
       const int32_t c = c_val[j];
       if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
@@ -57,6 +69,10 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
       if (maxc) atomicMax(&maxc[b], static_cast<uint32_t>(c));
     }
   }
+  __syncthreads();
+  if (lds_gmin)
+    for (int64_t i = threadIdx.x; i < T; i += kBlock)
+      if (gmin_s[i] != ~0ull) atomicMin(&gmin[i], gmin_s[i]);
 }
 
 // Buckets are padded to a multiple of 4 entries (16 B) so the hot kernel's
@@ -267,7 +283,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   if (tile_maxc) DPS_HIP_RET(hipMemsetAsync(tile_maxc, 0, (nb + 1) * sizeof(uint32_t), st));
   if (tile_gmin && T > 0) DPS_HIP_RET(hipMemsetAsync(tile_gmin, 0x7F, T * sizeof(int64_t), st));
   if (n_targets > 0 && nb > 0) {
-    k_tile_count<<<grid_for(n_targets * kWave, kBlock), kBlock, 0, st>>>(
+    k_tile_count<<<grid_for(n_targets * kWave, kBlock, 2048), kBlock, 0, st>>>(
         c_ptr, c_col, c_val, t_rank, g, n_targets, shift, T, cnt, tile_maxc,
         reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
     DPS_LAUNCHED();
