@@ -57,6 +57,10 @@ SIGNATURES = {
     "dps_walk_row": (C.c_int, [_p, _p, _i64, _p, _i64, _i64, _i32, _p, _p, _p, _p]),
     "dps_row_scores": (C.c_int, [_p, _p, _i64, _i64, _p, _p, _p]),
     "dps_pair_count": (C.c_int, [_p, _p, _i64, _p, _p, _i64, _p, _p]),
+    "dps_format_float": (C.c_int, [C.c_double, C.c_char_p, _sz]),
+    "dps_write_topk_log": (C.c_int, [C.c_char_p, C.c_int, _i64, _i64, _i32, _p, _p, _p, _p,
+                                     C.c_char_p, _p, C.c_char_p, _p, C.c_double, C.c_double,
+                                     C.c_int]),
 }
 
 

@@ -238,6 +238,30 @@ int dps_pair_count(const int32_t* a_col, const int32_t* a_val, int64_t a_len,
                    const int32_t* b_col, const int32_t* b_val, int64_t b_len,
                    int64_t* out, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * A8. Run-log format (DPathSim_APVPA.py:32-67), host-side, for all-pairs
+ * results.  Host arrays only (no device work, no GPU needed).
+ *
+ * dps_format_float: Python's repr() of a double (the reference formats scores
+ *   with '{}'.format(float), :47-49/:56-64) into out[cap] (NUL-terminated).
+ * dps_write_topk_log: for source rows x = row_begin + r, r < n_rows, writes
+ *   "Source author global walk: {g[x]}" and, for each ranked target y =
+ *   idx[r*k + s] >= 0 in rank order, the reference's five-line target block
+ *   ("Pairwise authors walk {id[y]}: {cnt}", "Target author global walk:
+ *   {g[y]}", "Sim score {label[x]} - {label[y]}: {score}", "***Stage done in:
+ *   {stage_seconds}", "---"); then "***Overall done in: {overall_seconds}" if
+ *   overall_seconds >= 0.  ids / labels: UTF-8 strings of every author ordinal,
+ *   concatenated in *_blob with offsets *_off[n_authors + 1].  g_host is indexed
+ *   by author ordinal.  append != 0 appends (the reference opens with 'a').
+ *   n_threads <= 0: all hardware threads.
+ * ------------------------------------------------------------------------- */
+int dps_format_float(double v, char* out, size_t cap);
+int dps_write_topk_log(const char* path, int append, int64_t row_begin, int64_t n_rows, int32_t k,
+                       const int32_t* idx_host, const int64_t* cnt_host, const double* score_host,
+                       const int64_t* g_host, const char* id_blob, const int64_t* id_off,
+                       const char* label_blob, const int64_t* label_off, double stage_seconds,
+                       double overall_seconds, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif
