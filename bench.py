@@ -53,7 +53,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dpathsim.dist import gather_topk, max_shard, shard_bounds
+    from dpathsim.dist import balanced_bounds, gather_topk, max_shard
     from dpathsim.engine import PathSimEngine
     from dpathsim.synth import CONFIGS, synth_config
 
@@ -73,9 +73,15 @@ def main():
     NA = typed.n_authors
 
     eng = PathSimEngine(typed, device=dev, tile_w=args.tile_w).upload()
-    r0, r1 = shard_bounds(NA, rank, world)       # contiguous balanced row shard
-    shard = r1 - r0
-    m = max_shard(NA, world)
+
+    def plan():
+        # contiguous row shards of equal estimated work (every rank derives the
+        # same bounds from its own, identical C: no communication)
+        return balanced_bounds(eng.row_work(), world) if world > 1 else [(0, NA)]
+
+    eng.build()
+    bounds0 = plan()
+    m = max_shard(NA, world, bounds0)
     out = (torch.empty((m, k), dtype=torch.int32, device=dev),
            torch.empty((m, k), dtype=torch.int64, device=dev),
            torch.empty((m, k), dtype=torch.float64, device=dev))
@@ -87,7 +93,11 @@ def main():
 
     def step(record):
         eng.build()
-        view = tuple(t[:shard] for t in out)
+        bounds = plan()
+        if bounds != bounds0:
+            raise RuntimeError("row shards changed between steps")
+        r0, r1 = bounds[rank]
+        view = tuple(t[:r1 - r0] for t in out)
         if record:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -97,7 +107,7 @@ def main():
             e1.record()
             ev_topk.append((e0, e1))
         if world > 1:
-            gather_topk(out, NA, world, out=gathered)
+            gather_topk(out, NA, world, out=gathered, bounds=bounds)
 
     for _ in range(args.warmup):
         step(False)
@@ -123,6 +133,8 @@ def main():
 
     # ---- roofline of the dominant kernel (dps_cct_topk), measured live --------
     topk_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_topk]))
+    r0, r1 = bounds0[rank]
+    shard = r1 - r0
     c_ptr = eng.tensor("c_ptr")
     nnz = eng.info.nnz_c
     c_col = eng.tensor("c_col")[:nnz].long()
@@ -189,7 +201,7 @@ def main():
                                    f"{typed.n_mids} {typed.metapath.mid_type}s, all-pairs top-{k}",
                        "n_authors": NA, "k": k, "tile_w": args.tile_w,
                        "nnz_C": info.nnz_c, "sum_terms": terms if world == 1 else None,
-                       "parallelism": f"row-shard x{world}"},
+                       "parallelism": f"row-shard x{world} (work-balanced, heaviest rows first)"},
             "roofline": {"bound": "hbm", "kernel": "dps_cct_topk", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes": bytes_launch,

@@ -148,6 +148,7 @@ struct CctParams {
   int64_t T;
   int shift;
   int64_t row_begin;
+  const int32_t* row_order;  // nullable: dequeue order of the rows (e.g. heaviest first)
   int64_t n_rows;
   int k;
   int32_t* out_idx;
@@ -649,7 +650,8 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     __syncthreads();
     const int64_t r = row_s;
     if (r >= p.n_rows) break;
-    const int64_t x = p.row_begin + r;
+    const int64_t x = p.row_order ? static_cast<int64_t>(p.row_order[r]) : p.row_begin + r;
+    const int64_t ro = x - p.row_begin;   // output row
     const int64_t x_lab = p.t_rank ? static_cast<int64_t>(p.t_rank[x]) : x;
     const int64_t pb = p.c_ptr[x];
     const int d = static_cast<int>(p.c_ptr[x + 1] - pb);
@@ -826,9 +828,9 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
       }
       // ranked entries, then zero-score targets in reference order, then -1
-      int32_t* oi = p.out_idx + r * p.k;
-      int64_t* oc = p.out_cnt + r * p.k;
-      double* os = p.out_score + r * p.k;
+      int32_t* oi = p.out_idx + ro * p.k;
+      int64_t* oc = p.out_cnt + ro * p.k;
+      double* os = p.out_score + ro * p.k;
 #pragma unroll
       for (int q = 0; q < KPL; ++q) {
         const int slot = q * kWave + lane;
@@ -909,7 +911,8 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
                  const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
                  const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                  const uint32_t* tile_off, const uint32_t* tile_ent, const uint32_t* tile_maxc,
-                 const int64_t* tile_gmin, int64_t row_begin, int64_t row_end, int32_t k,
+                 const int64_t* tile_gmin, int64_t row_begin, int64_t row_end,
+                 const int32_t* row_order, int32_t k,
                  int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
                  size_t ws_bytes, void* stream) {
   (void)n_mids;
@@ -939,7 +942,7 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   p.T = (n_targets + tile_w - 1) / tile_w;
   p.shift = shift;
   p.dbuf = shift <= 14;   // 2 x W bytes of u8 accumulators up to W = 16384, one 32 KB buffer above
-  p.row_begin = row_begin; p.n_rows = n_rows; p.k = k;
+  p.row_begin = row_begin; p.row_order = row_order; p.n_rows = n_rows; p.k = k;
   p.out_idx = out_idx; p.out_cnt = out_cnt; p.out_score = out_score;
   p.counter = static_cast<unsigned long long*>(ws);
   p.ablate = 0;

@@ -18,22 +18,49 @@ def shard_bounds(n_rows: int, rank: int, world: int) -> tuple[int, int]:
     return n_rows * rank // world, n_rows * (rank + 1) // world
 
 
-def max_shard(n_rows: int, world: int) -> int:
-    return max(b - a for a, b in (shard_bounds(n_rows, r, world) for r in range(world)))
+def max_shard(n_rows: int, world: int, bounds=None) -> int:
+    if bounds is None:
+        bounds = [shard_bounds(n_rows, r, world) for r in range(world)]
+    return max(b - a for a, b in bounds)
 
 
-def gather_topk(parts, n_rows: int, world: int, group=None, out=None):
+def balanced_bounds(work: torch.Tensor, world: int) -> list[tuple[int, int]]:
+    """Contiguous shards of (nearly) equal total work.
+
+    ``work``: per-row work estimate (int64, any device, e.g.
+    PathSimEngine.row_work()).  Rank r gets the rows whose work prefix falls in
+    [r/world, (r+1)/world) of the total.  Every rank computes the same bounds
+    from the same C, so no communication is needed.
+    """
+    n = int(work.numel())
+    if world < 1:
+        raise ValueError(f"bad world {world}")
+    if world == 1 or n == 0:
+        return [shard_bounds(n, r, world) for r in range(world)]
+    pre = torch.cumsum(work.to(torch.int64), 0)
+    total = pre[-1]
+    cuts = torch.arange(1, world, device=pre.device, dtype=torch.int64) * total // world
+    idx = torch.searchsorted(pre, cuts, right=True).cpu().tolist()
+    edges = [0] + [min(max(int(i), 0), n) for i in idx] + [n]
+    for i in range(1, len(edges)):
+        edges[i] = max(edges[i], edges[i - 1])
+    return [(edges[r], edges[r + 1]) for r in range(world)]
+
+
+def gather_topk(parts, n_rows: int, world: int, group=None, out=None, bounds=None):
     """All-gather every rank's top-k block into the full [n_rows, k] tensors.
 
     ``parts``: this rank's (idx, cnt, score) tensors with shape [max_shard, k]
     (rows past its shard are padding).  Returns (idx, cnt, score) for all
     n_rows rows in row order on every rank; ``out`` may hold preallocated
-    [world * max_shard, k] receive buffers (reused across steps).
+    [world * max_shard, k] receive buffers (reused across steps).  ``bounds``:
+    the shards in use (default: equal row counts, shard_bounds).
     """
+    if bounds is None:
+        bounds = [shard_bounds(n_rows, r, world) for r in range(world)]
     if world == 1:
-        r1 = shard_bounds(n_rows, 0, 1)[1]
-        return tuple(p[:r1] for p in parts)
-    m = max_shard(n_rows, world)
+        return tuple(p[:bounds[0][1]] for p in parts)
+    m = max_shard(n_rows, world, bounds)
     if out is None:
         out = tuple(torch.empty((world * m,) + tuple(p.shape[1:]), dtype=p.dtype, device=p.device)
                     for p in parts)
@@ -45,6 +72,5 @@ def gather_topk(parts, n_rows: int, world: int, group=None, out=None):
         else:
             dist.all_gather(list(dst.view(world, m, *src.shape[1:]).unbind(0)), src.contiguous(),
                             group=group)
-    rows = [slice(r * m, r * m + (b - a)) for r, (a, b) in
-            enumerate(shard_bounds(n_rows, r, world) for r in range(world))]
+    rows = [slice(r * m, r * m + (b - a)) for r, (a, b) in enumerate(bounds)]
     return tuple(torch.cat([o[s] for s in rows]) for o in out)

@@ -202,6 +202,7 @@ class PathSimEngine:
             torch.cuda.synchronize(self.device)
             for (a, ea), (b, eb) in zip(marks, marks[1:]):
                 info.phase_ms[b] = ea.elapsed_time(eb)
+        d.pop("row_work", None)
         d.update(ap_ptr=ap_ptr, ap_col=ap_col, px_ptr=px_ptr, px_col=px_col, c_ptr=c_ptr,
                  c_col=c_col, c_val=c_val, s=s, g=g, diag=diag, g_t=g_t, t_perm=t_perm,
                  t_rank=t_rank, tile_off=tile_off, tile_ent=tile_ent, tile_maxc=tile_maxc,
@@ -217,9 +218,32 @@ class PathSimEngine:
     def n_targets(self):
         return self.typed.n_authors
 
+    def row_work(self):
+        """Per-row work estimate of the hot kernel (device int64 [N_A]): the C^T
+        entries the row's venues hold, sum_{v in x} n_v, plus half the mean as a
+        stand-in for the per-stage fixed cost.  Used to order rows heaviest
+        first and to balance row shards across ranks."""
+        if "row_work" not in self._dev:
+            d = self._dev
+            NA, nnz = self.typed.n_authors, self.info.nnz_c
+            with torch.cuda.device(self.device):
+                col = d["c_col"][:nnz].long()
+                n_v = torch.bincount(col, minlength=self.typed.n_mids)
+                pre = torch.zeros(nnz + 1, dtype=torch.int64, device=self.device)
+                pre[1:] = torch.cumsum(n_v[col], 0)
+                ptr = d["c_ptr"][:NA + 1]
+                terms = pre[ptr[1:]] - pre[ptr[:-1]]
+                d["row_work"] = terms + (terms.sum() // max(NA, 1)) // 2
+        return self._dev["row_work"]
+
     # ------------------------------------------------------------------ top-k
-    def topk(self, k: int, row_begin: int = 0, row_end: int | None = None, out=None):
-        """★ all-pairs top-k for author rows [row_begin, row_end) (device tensors)."""
+    def topk(self, k: int, row_begin: int = 0, row_end: int | None = None, out=None,
+             heavy_first: bool = True):
+        """★ all-pairs top-k for author rows [row_begin, row_end) (device tensors).
+
+        ``heavy_first`` dequeues the rows in descending ``row_work`` order (LPT),
+        so the few very heavy rows do not trail at the end of the launch; the
+        results are identical either way."""
         if not self.built:
             raise RuntimeError("call build() first")
         NA = self.typed.n_authors
@@ -236,11 +260,15 @@ class PathSimEngine:
         if R == 0:
             return idx, cnt, sc
         with torch.cuda.device(self.device):
+            order = None
+            if heavy_first and R > 1:
+                w = self.row_work()[row_begin:row_end]
+                order = (torch.argsort(w, descending=True, stable=True) + row_begin).to(torch.int32)
             _lib.call("dps_cct_topk", _ptr(d["c_ptr"]), _ptr(d["c_col"]), _ptr(d["c_val"]),
                       _ptr(d["g"]), _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA,
                       self.typed.n_mids, self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
                       _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]),
-                      int(row_begin), int(row_end), int(k),
+                      int(row_begin), int(row_end), _ptr(order), int(k),
                       _ptr(idx), _ptr(cnt), _ptr(sc), _ptr(d["topk_ws"]), d["topk_ws"].numel(),
                       self.stream)
         return idx, cnt, sc

@@ -163,7 +163,7 @@ int dps_target_order(const int64_t* g, int64_t n_targets, int32_t key_bits,
 /* ---------------------------------------------------------------------------
  * A5 operand layout, step 2: target-tiled transpose of C for the C.C^T kernels.
  * Target labels (t_rank[y], or y if t_rank == NULL) in [0, n_targets) are cut
- * into tiles of `tile_w` (power of two, 256..16384; the hot kernel keeps
+ * into tiles of `tile_w` (power of two, 256..32768; the hot kernel keeps
  * acc int32[W] + bitmap + list uint16[W] of one tile in LDS per wave).
  * Bucket (v, t) holds the packed entries
  *   (C[y,v] << 16) | (label(y) - t*tile_w)   for every y of tile t with C[y,v] > 0,
@@ -200,8 +200,12 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
  * dps_target_order (all NULL = identity labels, g_t = g); tile_* from
  * dps_ct_tiles_build with the same t_rank (tile_gmin required, tile_maxc
  * optional -- enables skipping tiles that cannot hold a top-k candidate).
- * Outputs (row-major [row_end-row_begin][k]): out_idx int32 (original
- * ordinals), out_cnt int64 (M), out_score double.  1 <= k <= 256.
+ * Outputs (row-major [row_end-row_begin][k], output row x - row_begin):
+ * out_idx int32 (original ordinals), out_cnt int64 (M), out_score double.
+ * 1 <= k <= 256.  row_order (nullable, int32[row_end-row_begin]): a
+ * permutation of [row_begin, row_end) giving the order in which rows are
+ * dequeued (heaviest first keeps the kernel tail short); results never
+ * depend on it.
  * Requires max M[x,x] < 2^31.  ws: dps_cct_topk_workspace_size() bytes.
  * ------------------------------------------------------------------------- */
 size_t dps_cct_topk_workspace_size(void);
@@ -210,7 +214,7 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
                  const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                  const uint32_t* tile_off, const uint32_t* tile_ent,
                  const uint32_t* tile_maxc, const int64_t* tile_gmin,
-                 int64_t row_begin, int64_t row_end, int32_t k,
+                 int64_t row_begin, int64_t row_end, const int32_t* row_order, int32_t k,
                  int32_t* out_idx, int64_t* out_cnt, double* out_score,
                  void* ws, size_t ws_bytes, void* stream);
 

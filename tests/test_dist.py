@@ -12,7 +12,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from dpathsim.dist import gather_topk, max_shard, shard_bounds
+from dpathsim.dist import balanced_bounds, gather_topk, max_shard, shard_bounds
 
 
 @pytest.mark.parametrize("n", [0, 1, 7, 1000, 1_000_003])
@@ -33,7 +33,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, k, result_path):
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_balanced_bounds_partition_and_balance(world):
+    rng = np.random.default_rng(world)
+    w = torch.from_numpy(rng.pareto(1.2, 100_000).astype(np.int64) + 1)
+    b = balanced_bounds(w, world)
+    assert b[0][0] == 0 and b[-1][1] == len(w)
+    assert all(x[1] == y[0] for x, y in zip(b, b[1:]))
+    loads = [int(w[a:c].sum()) for a, c in b]
+    assert max(loads) - min(loads) <= 2 * int(w.max())    # balanced up to one row per cut
+    assert balanced_bounds(torch.zeros(0, dtype=torch.int64), world) == [(0, 0)] * world
+
+
+def _worker(rank, world, port, k, result_path, balanced=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -42,15 +54,21 @@ def _worker(rank, world, port, k, result_path):
         t = synth_dblp(1500, 4500, 120, seed=21).typed()
         co = po.COracle.from_typed(t)
         na = t.n_authors
-        r0, r1 = shard_bounds(na, rank, world)
-        m = max_shard(na, world)
+        bounds = None
+        if balanced:      # shards by per-row work sum_{v in x} n_v (as PathSimEngine.row_work)
+            cp, cc = co.export()[:2]
+            n_v = np.bincount(cc, minlength=t.n_mids)
+            pre = np.concatenate([[0], np.cumsum(n_v[cc])])
+            bounds = balanced_bounds(torch.from_numpy(pre[cp[1:]] - pre[cp[:-1]]), world)
+        r0, r1 = bounds[rank] if bounds else shard_bounds(na, rank, world)
+        m = max_shard(na, world, bounds)
         oi, oc, os_ = co.topk(k, r0, r1, threads=1)
         parts = []
         for a, dt in ((oi, torch.int32), (oc, torch.int64), (os_, torch.float64)):
             p = torch.zeros((m, k), dtype=dt)
             p[: r1 - r0] = torch.from_numpy(a)
             parts.append(p)
-        gi, gc, gs = gather_topk(tuple(parts), na, world)
+        gi, gc, gs = gather_topk(tuple(parts), na, world, bounds=bounds)
         if rank == 0:
             fi, fc, fs = co.topk(k, 0, na, threads=1)
             ok = (np.array_equal(gi.numpy(), fi) and np.array_equal(gc.numpy(), fc)
@@ -61,9 +79,10 @@ def _worker(rank, world, port, k, result_path):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("balanced", [False, True])
 @pytest.mark.parametrize("world", [2, 3])
-def test_gloo_gather_equals_single_rank(tmp_path, world):
+def test_gloo_gather_equals_single_rank(tmp_path, world, balanced):
     out = tmp_path / "result.txt"
-    mp.start_processes(_worker, args=(world, _free_port(), 10, str(out)), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), 10, str(out), balanced), nprocs=world,
                        join=True, start_method="spawn")
     assert out.read_text() == "ok"

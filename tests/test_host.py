@@ -131,10 +131,10 @@ def test_c_abi_rejects_bad_arguments_without_gpu():
     """Argument validation happens host-side before any HIP call."""
     lib = _lib.load()
     rc = lib.dps_cct_topk(None, None, None, None, None, None, None, 10, 5, 300, None, None,
-                          None, None, 0, 10, 10, None, None, None, None, 0, None)
+                          None, None, 0, 10, None, 10, None, None, None, None, 0, None)
     assert rc == _lib.DPS_ERR_UNSUPPORTED     # tile_w 300 is not a power of two
     assert b"tile_w" in lib.dps_last_error()
     rc = lib.dps_cct_topk(None, None, None, None, None, None, None, 10, 5, 256, None, None,
-                          None, None, 0, 10, 0, None, None, None, None, 0, None)
+                          None, None, 0, 10, None, 0, None, None, None, None, 0, None)
     assert rc == _lib.DPS_ERR_UNSUPPORTED     # k = 0
     assert lib.dps_csr_build_workspace_size(100, 10) > 0
