@@ -60,9 +60,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for the multi-rank path on a one-GPU box (never set by the
+    # driver): all ranks on one device, gloo instead of RCCL
+    local = int(os.environ.get("DPATHSIM_BENCH_DEVICE", local))
+    backend = os.environ.get("DPATHSIM_BENCH_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 

@@ -69,8 +69,11 @@ def gather_topk(parts, n_rows: int, world: int, group=None, out=None, bounds=Non
             raise ValueError(f"part has {src.shape[0]} rows, expected max_shard {m}")
         if dist.get_backend(group) == "nccl":
             dist.all_gather_into_tensor(dst, src.contiguous(), group=group)
-        else:
-            dist.all_gather(list(dst.view(world, m, *src.shape[1:]).unbind(0)), src.contiguous(),
-                            group=group)
+        else:   # gloo (CPU tests, one-GPU rehearsal): host staging
+            host = dst.cpu() if dst.is_cuda else dst
+            dist.all_gather(list(host.view(world, m, *src.shape[1:]).unbind(0)),
+                            src.contiguous().cpu(), group=group)
+            if host is not dst:
+                dst.copy_(host)
     rows = [slice(r * m, r * m + (b - a)) for r, (a, b) in enumerate(bounds)]
     return tuple(torch.cat([o[s] for s in rows]) for o in out)
