@@ -917,8 +917,8 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
                  size_t ws_bytes, void* stream) {
   (void)n_mids;
   const int shift = log2_exact(tile_w);
-  DPS_REQUIRE(shift >= 8 && shift <= 15, DPS_ERR_UNSUPPORTED,
-              "tile_w must be a power of two in [256, 32768], got %d", tile_w);
+  DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED,
+              "tile_w must be a power of two in [256, 65536], got %d", tile_w);
   DPS_REQUIRE(k >= 1 && k <= 256, DPS_ERR_UNSUPPORTED, "k must be in [1, 256], got %d", k);
   DPS_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= n_targets, DPS_ERR_INVALID,
               "row range [%lld, %lld) outside [0, %lld)", static_cast<long long>(row_begin),

@@ -258,8 +258,8 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
                        int64_t* tile_gmin, int32_t* status_dev, void* ws, size_t ws_bytes,
                        void* stream) {
   const int shift = log2_exact(tile_w);
-  DPS_REQUIRE(shift >= 8 && shift <= 15, DPS_ERR_UNSUPPORTED,
-              "tile_w must be a power of two in [256, 32768], got %d", tile_w);
+  DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED,
+              "tile_w must be a power of two in [256, 65536], got %d", tile_w);
   DPS_REQUIRE(n_targets >= 0 && n_mids >= 0, DPS_ERR_INVALID, "negative size");
   DPS_REQUIRE(n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "n_targets exceeds int32");
   DPS_REQUIRE(!tile_gmin || g, DPS_ERR_INVALID, "tile_gmin needs g");

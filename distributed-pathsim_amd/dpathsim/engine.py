@@ -50,8 +50,8 @@ class PathSimEngine:
         _lib.load()
         self.typed = typed
         self.device = torch.device(device if device is not None else "cuda")
-        if tile_w & (tile_w - 1) or not 256 <= tile_w <= 32768:
-            raise ValueError("tile_w must be a power of two in [256, 32768]")
+        if tile_w & (tile_w - 1) or not 256 <= tile_w <= 65536:
+            raise ValueError("tile_w must be a power of two in [256, 65536]")
         self.tile_w = int(tile_w)
         self.tile_skip = True
         self.info = BuildInfo()
