@@ -128,6 +128,103 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restri
 }
 
 // --------------------------------------------------------------------------
+// Block-local tile build (n_mids <= kBlkMids): a block owns a contiguous range
+// of kBlkLabels target labels -- all inside one tile -- and counts its entries
+// per venue in LDS, so the hot buckets of heavy venues take one global atomic
+// per block instead of one per entry.  The scatter pass reserves each venue's
+// range with one global atomicAdd per (block, venue) and places entries with
+// LDS cursors.  Entry order inside a bucket is unspecified either way.
+constexpr int kBlkMids = 8192;
+constexpr int kBlkLabels = 1024;
+
+__global__ __launch_bounds__(kBlock) void k_tile_invert(const int32_t* __restrict__ rank,
+                                                        int64_t n, int32_t* __restrict__ perm) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kBlock)
+    perm[rank[i]] = static_cast<int32_t>(i);
+}
+
+__device__ __forceinline__ int64_t row_of_label(const int32_t* perm, int64_t lab) {
+  return perm ? static_cast<int64_t>(perm[lab]) : lab;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_count_blk(
+    const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
+    const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm,
+    const int64_t* __restrict__ g, int64_t n_targets, int64_t n_mids, int shift, int64_t T,
+    int labels_per_block, uint32_t* __restrict__ cnt, uint32_t* __restrict__ maxc,
+    unsigned long long* __restrict__ gmin, int32_t* __restrict__ status) {
+  __shared__ uint32_t cnt_s[kBlkMids];
+  __shared__ uint32_t mx_s[kBlkMids];
+  __shared__ unsigned long long gmin_s;
+  for (int64_t v = threadIdx.x; v < n_mids; v += kBlock) { cnt_s[v] = 0; mx_s[v] = 0; }
+  if (threadIdx.x == 0) gmin_s = ~0ull;
+  __syncthreads();
+  const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
+  const int64_t l0 = static_cast<int64_t>(blockIdx.x) * labels_per_block;
+  const int64_t l1 = min(l0 + labels_per_block, n_targets);
+  const int64_t t = l0 >> shift;
+  unsigned long long gm = ~0ull;
+  for (int64_t lab = l0 + wave; lab < l1; lab += kWavesPerBlock) {
+    const int64_t y = row_of_label(perm, lab);
+    if (g) gm = min(gm, static_cast<unsigned long long>(g[y]));
+    for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
+      const int32_t c = c_val[j];
+      if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
+      const int32_t v = c_col[j];
+      atomicAdd(&cnt_s[v], 1u);
+      atomicMax(&mx_s[v], static_cast<uint32_t>(c));
+    }
+  }
+  if (lane == 0 && gm != ~0ull) atomicMin(&gmin_s, gm);
+  __syncthreads();
+  for (int64_t v = threadIdx.x; v < n_mids; v += kBlock) {
+    if (!cnt_s[v]) continue;
+    atomicAdd(&cnt[v * T + t], cnt_s[v]);
+    if (maxc) atomicMax(&maxc[v * T + t], mx_s[v]);
+  }
+  if (threadIdx.x == 0 && gmin && gmin_s != ~0ull) atomicMin(&gmin[t], gmin_s);
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_scatter_blk(
+    const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
+    const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm, int64_t n_targets,
+    int64_t n_mids, int shift, int64_t T, int labels_per_block,
+    const int64_t* __restrict__ off, uint32_t* __restrict__ cursor, uint32_t* __restrict__ ent) {
+  __shared__ uint32_t cnt_s[kBlkMids];
+  __shared__ uint32_t base_s[kBlkMids];
+  for (int64_t v = threadIdx.x; v < n_mids; v += kBlock) cnt_s[v] = 0;
+  __syncthreads();
+  const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
+  const int64_t l0 = static_cast<int64_t>(blockIdx.x) * labels_per_block;
+  const int64_t l1 = min(l0 + labels_per_block, n_targets);
+  const int64_t t = l0 >> shift;
+  const uint32_t ymask = (1u << shift) - 1u;
+  for (int64_t lab = l0 + wave; lab < l1; lab += kWavesPerBlock) {
+    const int64_t y = row_of_label(perm, lab);
+    for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) atomicAdd(&cnt_s[c_col[j]], 1u);
+  }
+  __syncthreads();
+  for (int64_t v = threadIdx.x; v < n_mids; v += kBlock) {
+    const uint32_t n = cnt_s[v];
+    base_s[v] = n ? atomicAdd(&cursor[v * T + t], n) : 0u;
+    cnt_s[v] = 0;
+  }
+  __syncthreads();
+  for (int64_t lab = l0 + wave; lab < l1; lab += kWavesPerBlock) {
+    const int64_t y = row_of_label(perm, lab);
+    for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
+      const int32_t v = c_col[j];
+      const uint32_t pos = base_s[v] + atomicAdd(&cnt_s[v], 1u);
+      ent[off[v * T + t] + pos] =
+          (static_cast<uint32_t>(c_val[j]) << 16) | (static_cast<uint32_t>(lab) & ymask);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
 // Single-source dense row: one block per target tile; out_m in ORIGINAL order.
 __global__ __launch_bounds__(kBlock) void k_walk_row(const int32_t* __restrict__ src_col,
                                                      const int32_t* __restrict__ src_val,
@@ -136,24 +233,31 @@ __global__ __launch_bounds__(kBlock) void k_walk_row(const int32_t* __restrict__
                                                      const uint32_t* __restrict__ ent,
                                                      const int32_t* __restrict__ t_perm,
                                                      int64_t* __restrict__ out_m) {
+  // int32 accumulators for up to 32768 labels; wider tiles run in 32768-label parts
   extern __shared__ __attribute__((aligned(16))) int32_t acc[];
   const int W = 1 << shift;
+  const int P = W < 32768 ? W : 32768;
   const int64_t t = blockIdx.x;
-  for (int i = threadIdx.x; i < W; i += kBlock) acc[i] = 0;
-  __syncthreads();
-  for (int64_t j = 0; j < src_len; ++j) {
-    const int64_t b = static_cast<int64_t>(src_col[j]) * T + t;
-    const int cx = src_val[j];
-    for (uint32_t i = off[b] + threadIdx.x; i < off[b + 1]; i += kBlock) {
-      const uint32_t e = ent[i];
-      atomicAdd(&acc[e & 0xFFFFu], cx * static_cast<int>(e >> 16));
+  for (int part = 0; part < W / P; ++part) {
+    for (int i = threadIdx.x; i < P; i += kBlock) acc[i] = 0;
+    __syncthreads();
+    for (int64_t j = 0; j < src_len; ++j) {
+      const int64_t b = static_cast<int64_t>(src_col[j]) * T + t;
+      const int cx = src_val[j];
+      for (uint32_t i = off[b] + threadIdx.x; i < off[b + 1]; i += kBlock) {
+        const uint32_t e = ent[i];
+        const uint32_t lab = e & 0xFFFFu;
+        if (static_cast<int>(lab) / P != part) continue;
+        atomicAdd(&acc[lab % P], cx * static_cast<int>(e >> 16));
+      }
     }
-  }
-  __syncthreads();
-  const int64_t y0 = t << shift;
-  for (int i = threadIdx.x; i < W && y0 + i < n_targets; i += kBlock) {
-    const int64_t lab = y0 + i;
-    out_m[t_perm ? t_perm[lab] : lab] = acc[i];
+    __syncthreads();
+    const int64_t y0 = (t << shift) + static_cast<int64_t>(part) * P;
+    for (int i = threadIdx.x; i < P && y0 + i < n_targets; i += kBlock) {
+      const int64_t lab = y0 + i;
+      out_m[t_perm ? t_perm[lab] : lab] = acc[i];
+    }
+    __syncthreads();
   }
 }
 
@@ -249,6 +353,7 @@ size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t ti
   s += align_up(static_cast<size_t>(nb + 1) * sizeof(uint32_t));  // cursor
   s += align_up(static_cast<size_t>(nb + 1) * sizeof(int64_t));   // off64
   s += align_up(scan_workspace_size(nb + 1));
+  s += align_up(static_cast<size_t>(n_targets > 0 ? n_targets : 1) * sizeof(int32_t));  // perm
   return s + 1024;
 }
 
@@ -276,13 +381,27 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   int64_t* off64 = c.take<int64_t>(nb + 1);
   const size_t scan_ws = scan_workspace_size(nb + 1);
   void* sws = c.take<char>(scan_ws);
+  int32_t* perm = c.take<int32_t>(n_targets > 0 ? n_targets : 1);
   DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "tiles workspace carve failed");
+  const bool blk = n_mids <= kBlkMids;   // block-local LDS counting
+  const int lpb = tile_w < kBlkLabels ? tile_w : kBlkLabels;
+  const int64_t nblk = (n_targets + lpb - 1) / lpb;
+  if (blk && t_rank && n_targets > 0) {
+    k_tile_invert<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(t_rank, n_targets, perm);
+    DPS_LAUNCHED();
+  }
+  const int32_t* perm_or_null = t_rank ? perm : nullptr;
   if (status_dev) DPS_HIP_RET(hipMemsetAsync(status_dev, 0, sizeof(int32_t), st));
   DPS_HIP_RET(hipMemsetAsync(cnt, 0, (nb + 1) * sizeof(uint32_t), st));
   DPS_HIP_RET(hipMemsetAsync(cursor, 0, (nb + 1) * sizeof(uint32_t), st));
   if (tile_maxc) DPS_HIP_RET(hipMemsetAsync(tile_maxc, 0, (nb + 1) * sizeof(uint32_t), st));
   if (tile_gmin && T > 0) DPS_HIP_RET(hipMemsetAsync(tile_gmin, 0x7F, T * sizeof(int64_t), st));
-  if (n_targets > 0 && nb > 0) {
+  if (n_targets > 0 && nb > 0 && blk) {
+    k_tile_count_blk<<<static_cast<unsigned>(nblk), kBlock, 0, st>>>(
+        c_ptr, c_col, c_val, perm_or_null, tile_gmin ? g : nullptr, n_targets, n_mids, shift, T,
+        lpb, cnt, tile_maxc, reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
+    DPS_LAUNCHED();
+  } else if (n_targets > 0 && nb > 0) {
     k_tile_count<<<grid_for(n_targets * kWave, kBlock, 2048), kBlock, 0, st>>>(
         c_ptr, c_col, c_val, t_rank, g, n_targets, shift, T, cnt, tile_maxc,
         reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
@@ -295,7 +414,12 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, off64, nb, sws, scan_ws, st));
   k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, nb, tile_off);
   DPS_LAUNCHED();
-  if (n_targets > 0 && nb > 0) {
+  if (n_targets > 0 && nb > 0 && blk) {
+    k_tile_scatter_blk<<<static_cast<unsigned>(nblk), kBlock, 0, st>>>(
+        c_ptr, c_col, c_val, perm_or_null, n_targets, n_mids, shift, T, lpb, off64, cursor,
+        tile_ent);
+    DPS_LAUNCHED();
+  } else if (n_targets > 0 && nb > 0) {
     k_tile_scatter<<<grid_for(n_targets * kWave, kBlock), kBlock, 0, st>>>(
         c_ptr, c_col, c_val, t_rank, n_targets, shift, T, off64, cursor, tile_ent);
     DPS_LAUNCHED();
@@ -314,15 +438,17 @@ int dps_walk_row(const int32_t* src_col, const int32_t* src_val, int64_t src_len
                  void* stream) {
   (void)n_mids;
   const int shift = log2_exact(tile_w);
-  DPS_REQUIRE(shift >= 8 && shift <= 15, DPS_ERR_UNSUPPORTED, "bad tile_w %d", tile_w);
+  DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED, "bad tile_w %d", tile_w);
   DPS_REQUIRE(src_len >= 0 && n_targets >= 0, DPS_ERR_INVALID, "negative size");
   auto st = static_cast<hipStream_t>(stream);
   const int64_t T = (n_targets + tile_w - 1) / tile_w;
   if (T == 0) return DPS_OK;
   DPS_HIP_RET(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_walk_row),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(tile_w * sizeof(int32_t))));
-  k_walk_row<<<static_cast<unsigned>(T), kBlock, static_cast<size_t>(tile_w) * sizeof(int32_t),
+                                  static_cast<int>((tile_w < 32768 ? tile_w : 32768) *
+                                                   sizeof(int32_t))));
+  k_walk_row<<<static_cast<unsigned>(T), kBlock,
+               static_cast<size_t>(tile_w < 32768 ? tile_w : 32768) * sizeof(int32_t),
                st>>>(src_col, src_val, src_len, n_targets, shift, T, tile_off, tile_ent, t_perm,
                      out_m);
   DPS_LAUNCHED();

@@ -63,11 +63,16 @@ def test_tile_skip_does_not_change_results(dblp_small_tuples, dblp_small_expecte
     assert np.array_equal(sc.cpu().numpy().view(np.int64), ex["top10_score"].view(np.int64))
 
 
-def test_single_source_walks_match_oracle(small_engine, dblp_small_tuples):
+@pytest.mark.parametrize("tile_w", [256, 65536])
+def test_single_source_walks_match_oracle(dblp_small_tuples, tile_w):
+    """dps_walk_row / dps_pair_count / global walk; W = 65536 runs walk_row in
+    two 32768-label parts."""
     import pathsim_oracle as po
+    from dpathsim.engine import build_engine
+    from dpathsim.graph import Graph
     v, e = dblp_small_tuples
     og = po.OracleGraph(v, e)
-    eng = small_engine
+    eng = build_engine(Graph.from_tuples(v, e).typed(), tile_w=tile_w)
     t = eng.typed
     graph = t.graph
     rng = np.random.default_rng(1)
