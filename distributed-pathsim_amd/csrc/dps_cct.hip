@@ -108,9 +108,14 @@ struct TopK {
     int uy[KPL], um[KPL];
 #pragma unroll
     for (int r = 0; r < KPL; ++r) {
-      us[r] = __shfl_up(s[r], 1, kWave);
-      uy[r] = __shfl_up(y[r], 1, kWave);
-      um[r] = __shfl_up(m[r], 1, kWave);
+      // lane i <- lane i-1 with a DPP wave shift (no LDS round trip)
+      const uint64_t sb = static_cast<uint64_t>(__double_as_longlong(s[r]));
+      const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(sb), 0x138, 0xF, 0xF, false);
+      const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(sb >> 32), 0x138, 0xF, 0xF, false);
+      us[r] = __longlong_as_double(static_cast<long long>(
+          (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo)));
+      uy[r] = __builtin_amdgcn_update_dpp(0, y[r], 0x138, 0xF, 0xF, false);
+      um[r] = __builtin_amdgcn_update_dpp(0, m[r], 0x138, 0xF, 0xF, false);
       if (r > 0 && lane == 0) {
         us[r] = readlane(s[r - 1], kWave - 1);
         uy[r] = readlane(y[r - 1], kWave - 1);
@@ -572,6 +577,7 @@ __device__ __forceinline__ void epilogue(const CctParams& p, uint32_t* acc, TopK
 struct Window {
   int64_t tw;
   int v, c;
+  uint32_t vT;   // v * T: first bucket of venue v
   uint32_t lo, hi, mx;
 };
 
@@ -592,7 +598,7 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
     int64_t ub = ub32 >= (1u << 25) ? (int64_t(1) << 40) : static_cast<int64_t>(ub32);
     w.lo = hi;
     if (lane < d && t + 1 < p.T) {
-      const int64_t vb = static_cast<int64_t>(w.v) * p.T + t + 1;
+      const uint32_t vb = w.vT + static_cast<uint32_t>(t) + 1u;   // < V*T + 1 < 2^32
       w.hi = p.tile_off[vb + 1];
       w.mx = p.tile_maxc[vb];
     }
@@ -669,10 +675,12 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       w.tw = 0;
       w.v = 0; w.c = 0;
       w.lo = w.hi = w.mx = 0;
+      w.vT = 0;
       if (lane < d) {
         w.v = p.c_col[pb + lane];
         w.c = p.c_val[pb + lane];
-        const int64_t vb = static_cast<int64_t>(w.v) * p.T;
+        w.vT = static_cast<uint32_t>(w.v) * static_cast<uint32_t>(p.T);
+        const int64_t vb = w.vT;
         w.lo = p.tile_off[vb];
         w.hi = p.tile_off[vb + 1];
         w.mx = p.tile_maxc[vb];
@@ -915,7 +923,6 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
                  const int32_t* row_order, int32_t k,
                  int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
                  size_t ws_bytes, void* stream) {
-  (void)n_mids;
   const int shift = log2_exact(tile_w);
   DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED,
               "tile_w must be a power of two in [256, 65536], got %d", tile_w);
@@ -924,6 +931,8 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
               "row range [%lld, %lld) outside [0, %lld)", static_cast<long long>(row_begin),
               static_cast<long long>(row_end), static_cast<long long>(n_targets));
   DPS_REQUIRE(n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "n_targets exceeds int32");
+  DPS_REQUIRE(n_mids * ((n_targets + tile_w - 1) / tile_w) < int64_t(UINT32_MAX), DPS_ERR_OVERFLOW,
+              "n_mids * tiles exceeds the 32-bit bucket index");
   DPS_REQUIRE(!t_perm == !t_rank, DPS_ERR_INVALID, "t_perm and t_rank go together");
   DPS_REQUIRE(tile_gmin && g && tile_off && tile_ent, DPS_ERR_INVALID,
               "g, tile_off, tile_ent and tile_gmin are required");

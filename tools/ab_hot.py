@@ -12,6 +12,7 @@ from dpathsim.synth import synth_config
 from dpathsim.engine import build_engine
 
 R = int(os.environ.get("AB_ROWS", "200000"))
+K = int(os.environ.get("AB_K", "10"))
 Ws = [int(w) for w in os.environ.get("AB_W", "8192,16384").split(",")]
 ablations = [a for a in os.environ.get("AB_ABLATE", "1,2,4").split(",") if a]
 t = synth_config(os.environ.get("AB_CONFIG", "config3")).typed()
@@ -21,14 +22,14 @@ ref = None
 
 def timed(eng, rows):
     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(); o = eng.topk(10, 0, rows); e1.record(); torch.cuda.synchronize()
+    e0.record(); o = eng.topk(K, 0, rows); e1.record(); torch.cuda.synchronize()
     return e0.elapsed_time(e1), o
 
 
 for W in Ws:
     eng = build_engine(t, tile_w=W)
     os.environ["DPATHSIM_ABLATE"] = "0"
-    eng.topk(10, 0, 20000); torch.cuda.synchronize()
+    eng.topk(K, 0, 20000); torch.cuda.synchronize()
     ms, o = timed(eng, R)
     o = [a.cpu().numpy() for a in o]
     res[f"W{W}"] = ms
