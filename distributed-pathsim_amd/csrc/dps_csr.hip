@@ -112,35 +112,51 @@ __global__ __launch_bounds__(kBlock) void k_seg_short(int32_t* __restrict__ data
                                                       int64_t n_seg, int64_t* __restrict__ uniq,
                                                       int32_t* __restrict__ long_list,
                                                       unsigned* __restrict__ n_long) {
+  // Triage 64 segments per wave, one per lane (coalesced seg_ptr reads): empty
+  // and single-element segments are finished by their lane, long ones (> 64)
+  // go to the block-level kernel, and the rest are sorted one at a time by the
+  // whole wave.  Most segments of the typed CSR builds are empty (non-author
+  // rows) or single (one venue per paper).
   const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
-  for (int64_t s = wave0; s < n_seg; s += nwaves) {
-    const int64_t beg = seg_ptr[s];
-    const int len = static_cast<int>(seg_ptr[s + 1] - beg);
-    if (len > kWave) {
-      if (lane == 0) long_list[atomicAdd(n_long, 1u)] = static_cast<int32_t>(s);
-      continue;
-    }
-    if (len == 0) {
-      if (lane == 0) uniq[s] = 0;
-      continue;
-    }
-    int v = lane < len ? data[beg + lane] : INT_MAX;
-    v = wave_bitonic_sort(v);
-    const int prev = __shfl_up(v, 1, kWave);
-    const bool first = lane < len && (lane == 0 || v != prev);
-    const uint64_t mask = ballot(first);
-    if (first) {
-      const int rank = mbcnt(mask);
-      data[beg + rank] = v;
-      if (counts) {
-        const uint64_t above = mask & ~((2ull << lane) - 1ull);
-        const int next = above ? (__ffsll(static_cast<long long>(above)) - 1) : len;
-        counts[beg + rank] = next - lane;
+  for (int64_t s0 = wave0 * kWave; s0 < n_seg; s0 += nwaves * kWave) {
+    const int64_t sl = s0 + lane;
+    int64_t bl = 0;
+    int ll = 0;
+    if (sl < n_seg) {
+      bl = seg_ptr[sl];
+      ll = static_cast<int>(seg_ptr[sl + 1] - bl);
+      if (ll <= 1) {
+        uniq[sl] = ll;
+        if (ll == 1 && counts) counts[bl] = 1;
+      } else if (ll > kWave) {
+        long_list[atomicAdd(n_long, 1u)] = static_cast<int32_t>(sl);
       }
     }
-    if (lane == 0) uniq[s] = __popcll(mask);
+    uint64_t todo = ballot(ll >= 2 && ll <= kWave);
+    while (todo) {
+      const int src = __ffsll(static_cast<long long>(todo)) - 1;
+      todo &= todo - 1;
+      const int64_t s = s0 + src;
+      const int64_t beg = readlane(bl, src);
+      const int len = readlane(ll, src);
+      int v = lane < len ? data[beg + lane] : INT_MAX;
+      v = wave_bitonic_sort(v);
+      const int prev = __shfl_up(v, 1, kWave);
+      const bool first = lane < len && (lane == 0 || v != prev);
+      const uint64_t mask = ballot(first);
+      if (first) {
+        const int rank = mbcnt(mask);
+        data[beg + rank] = v;
+        if (counts) {
+          const uint64_t above = mask & ~((2ull << lane) - 1ull);
+          const int next = above ? (__ffsll(static_cast<long long>(above)) - 1) : len;
+          counts[beg + rank] = next - lane;
+        }
+      }
+      if (lane == 0) uniq[s] = __popcll(mask);
+    }
   }
 }
 
@@ -261,16 +277,33 @@ __global__ __launch_bounds__(kBlock) void k_compact(const int32_t* __restrict__ 
                                                     const int64_t* __restrict__ out_ptr,
                                                     int64_t n_seg, int32_t* __restrict__ col,
                                                     int32_t* __restrict__ val) {
+  // lane per segment for short ones (<= 8 heads), whole wave for the rest
   const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
-  for (int64_t s = wave0; s < n_seg; s += nwaves) {
-    const int64_t src = seg_ptr[s];
-    const int64_t dst = out_ptr[s];
-    const int64_t len = out_ptr[s + 1] - dst;
-    for (int64_t i = lane; i < len; i += kWave) {
-      col[dst + i] = tmp[src + i];
-      if (val) val[dst + i] = tmp_cnt[src + i];
+  for (int64_t s0 = wave0 * kWave; s0 < n_seg; s0 += nwaves * kWave) {
+    const int64_t sl = s0 + lane;
+    int64_t src = 0, dst = 0, len = 0;
+    if (sl < n_seg) {
+      src = seg_ptr[sl];
+      dst = out_ptr[sl];
+      len = out_ptr[sl + 1] - dst;
+      if (len <= 8) {
+        for (int64_t i = 0; i < len; ++i) {
+          col[dst + i] = tmp[src + i];
+          if (val) val[dst + i] = tmp_cnt[src + i];
+        }
+      }
+    }
+    uint64_t todo = ballot(len > 8);
+    while (todo) {
+      const int l = __ffsll(static_cast<long long>(todo)) - 1;
+      todo &= todo - 1;
+      const int64_t so = readlane(src, l), d0 = readlane(dst, l), n = readlane(len, l);
+      for (int64_t i = lane; i < n; i += kWave) {
+        col[d0 + i] = tmp[so + i];
+        if (val) val[d0 + i] = tmp_cnt[so + i];
+      }
     }
   }
 }
@@ -290,22 +323,47 @@ __global__ __launch_bounds__(kBlock) void k_expand_len(const int64_t* __restrict
                                                        const int64_t* __restrict__ px_ptr,
                                                        int64_t* __restrict__ e_len,
                                                        unsigned long long* e_total) {
+  // lane per output row for rows of <= 32 papers, whole wave for longer rows;
+  // one atomic per wave for the total
   const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
-  int64_t wave_total = 0;   // one atomic per wave, not per row
-  for (int64_t i = wave0; i < n_out; i += nwaves) {
-    const int64_t r = out_row_src(rows, i);
-    const int64_t b = ap_ptr[r], e = ap_ptr[r + 1];
-    int64_t sum = 0;
-    for (int64_t j = b + lane; j < e; j += kWave) {
-      const int32_t p = ap_col[j];
-      sum += px_ptr[p + 1] - px_ptr[p];
+  int64_t lane_total = 0;
+  for (int64_t i0 = wave0 * kWave; i0 < n_out; i0 += nwaves * kWave) {
+    const int64_t i = i0 + lane;
+    int64_t b = 0, e = 0;
+    if (i < n_out) {
+      const int64_t r = out_row_src(rows, i);
+      b = ap_ptr[r];
+      e = ap_ptr[r + 1];
+      if (e - b <= 32) {
+        int64_t sum = 0;
+        for (int64_t j = b; j < e; ++j) {
+          const int32_t p = ap_col[j];
+          sum += px_ptr[p + 1] - px_ptr[p];
+        }
+        lane_total += sum;
+        if (e_len) e_len[i] = sum;
+      }
     }
-    sum = wave_sum(sum);
-    wave_total += sum;
-    if (lane == 0 && e_len) e_len[i] = sum;
+    uint64_t todo = ballot(e - b > 32);
+    while (todo) {
+      const int l = __ffsll(static_cast<long long>(todo)) - 1;
+      todo &= todo - 1;
+      const int64_t bb = readlane(b, l), ee = readlane(e, l);
+      int64_t sum = 0;
+      for (int64_t j = bb + lane; j < ee; j += kWave) {
+        const int32_t p = ap_col[j];
+        sum += px_ptr[p + 1] - px_ptr[p];
+      }
+      sum = wave_sum(sum);
+      if (lane == 0) {
+        lane_total += sum;
+        if (e_len) e_len[i0 + l] = sum;
+      }
+    }
   }
+  const int64_t wave_total = wave_sum(lane_total);
   if (lane == 0 && e_total && wave_total)
     atomicAdd(e_total, static_cast<unsigned long long>(wave_total));
 }
@@ -437,7 +495,7 @@ hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, in
   hipError_t e = hipMemsetAsync(n_long, 0, sizeof(unsigned), stream);
   if (e != hipSuccess) return e;
   if (n_seg <= 0) return hipSuccess;
-  k_seg_short<<<grid_for(n_seg * kWave, kBlock), kBlock, 0, stream>>>(data, counts, seg_ptr,
+  k_seg_short<<<grid_for(n_seg, kBlock), kBlock, 0, stream>>>(data, counts, seg_ptr,
                                                                       n_seg, uniq, long_list,
                                                                       n_long);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -530,7 +588,7 @@ int dps_csr_build(const int32_t* rows, const int32_t* cols, int64_t n_pairs,
   DPS_HIP_RET(seg_unique(tmp, nullptr, seg_ptr, n_rows, uniq, gws, seg_ws, st));
   DPS_HIP_RET(scan_exclusive<int64_t>(uniq, row_ptr, n_rows, sws, scan_ws, st));
   if (n_rows > 0) {
-    k_compact<<<grid_for(n_rows * kWave, kBlock), kBlock, 0, st>>>(tmp, nullptr, seg_ptr, row_ptr,
+    k_compact<<<grid_for(n_rows, kBlock), kBlock, 0, st>>>(tmp, nullptr, seg_ptr, row_ptr,
                                                                    n_rows, col_out, nullptr);
     DPS_LAUNCHED();
   }
@@ -547,7 +605,7 @@ int dps_spgemm_expand_size(const int64_t* ap_ptr, const int32_t* ap_col, const i
   auto st = static_cast<hipStream_t>(stream);
   DPS_HIP_RET(hipMemsetAsync(e_total, 0, sizeof(int64_t), st));
   if (n_out_rows == 0) return DPS_OK;
-  k_expand_len<<<grid_for(n_out_rows * kWave, kBlock), kBlock, 0, st>>>(
+  k_expand_len<<<grid_for(n_out_rows, kBlock), kBlock, 0, st>>>(
       ap_ptr, ap_col, rows, n_out_rows, px_ptr, nullptr,
       reinterpret_cast<unsigned long long*>(e_total));
   DPS_LAUNCHED();
@@ -597,7 +655,7 @@ int dps_spgemm_count(const int64_t* ap_ptr, const int32_t* ap_col, const int32_t
 
   if (c_col == nullptr) {  // symbolic: expand, sort, unique+count; keep results in ws
     if (n_out_rows > 0) {
-      k_expand_len<<<grid_for(n_out_rows * kWave, kBlock), kBlock, 0, st>>>(
+      k_expand_len<<<grid_for(n_out_rows, kBlock), kBlock, 0, st>>>(
           ap_ptr, ap_col, rows, n_out_rows, px_ptr, e_len, nullptr);
       DPS_LAUNCHED();
     }
@@ -614,7 +672,7 @@ int dps_spgemm_count(const int64_t* ap_ptr, const int32_t* ap_col, const int32_t
     return DPS_OK;
   }
   if (n_out_rows > 0) {  // numeric: compact (workspace of the symbolic call, unmodified)
-    k_compact<<<grid_for(n_out_rows * kWave, kBlock), kBlock, 0, st>>>(tmp, cnt, exp_ptr, c_ptr,
+    k_compact<<<grid_for(n_out_rows, kBlock), kBlock, 0, st>>>(tmp, cnt, exp_ptr, c_ptr,
                                                                        n_out_rows, c_col, c_val);
     DPS_LAUNCHED();
   }
