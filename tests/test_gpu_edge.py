@@ -1,0 +1,136 @@
+"""GPU edge cases and full-size output properties (HIP path vs the oracle).
+
+* degenerate graphs: one author (no targets: every slot empty), authors without
+  papers (g = 0: 0/0 scores 0.0 and the zero-score fill), k larger than the
+  number of targets (fill in reference order, then -1), no venue edges at all;
+* random multigraphs with the reference's corner cases (parallel edges,
+  author_of from non-author sources, papers with 0 or 2+ venues, self loops),
+  for k in the one-slot-per-lane (k <= 64) and two-slot (k > 64) top-k paths;
+* row slices and the dequeue order do not change any result;
+* config3 at full size (all 1M rows): per-row properties that do not need the
+  oracle -- scores non-increasing, ties by ascending ordinal, no self, distinct
+  targets -- plus sampled (row, slot) entries re-derived bit-exactly from
+  dps_pair_count and the global walks.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(v, e, k, tile_w=256):
+    import pathsim_oracle as po
+    from dpathsim.engine import build_engine
+    from dpathsim.graph import Graph
+    t = Graph.from_tuples(v, e).typed()
+    if t.n_authors == 0:
+        return None
+    eng = build_engine(t, tile_w=tile_w)
+    got = [a.cpu().numpy() for a in eng.topk(k)]
+    want = po.allpairs_topk(po.OracleGraph(v, e), k)
+    return got, want
+
+
+def _same(got, want):
+    gi, gc, gs = got
+    oi, oc, os_ = want
+    assert np.array_equal(gi, oi), (gi, oi)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(gs.view(np.int64), os_.view(np.int64))
+
+
+def test_single_author_has_no_targets():
+    v = [("a", "A", "author"), ("p", "P", "paper"), ("v", "V", "venue")]
+    e = [("a", "p", "author_of"), ("p", "v", "submit_at")]
+    got, want = _run(v, e, 5)
+    _same(got, want)
+    assert (got[0] == -1).all()
+
+
+def test_authors_without_papers_and_large_k():
+    v = [(f"a{i}", f"A{i}", "author") for i in range(6)] + \
+        [("p0", "P0", "paper"), ("p1", "P1", "paper"), ("v0", "V0", "venue")]
+    e = [("a0", "p0", "author_of"), ("a1", "p0", "author_of"), ("a2", "p1", "author_of"),
+         ("p0", "v0", "submit_at"), ("p1", "v0", "submit_at")]
+    for k in (1, 3, 5, 9):        # 5 targets per source; k = 9 leaves 4 empty slots
+        got, want = _run(v, e, k)
+        _same(got, want)
+    assert (got[0][:, 5:] == -1).all()
+
+
+def test_no_venue_edges():
+    v = [(f"a{i}", f"A{i}", "author") for i in range(4)] + [("p0", "P0", "paper")]
+    e = [("a0", "p0", "author_of"), ("a1", "p0", "author_of")]
+    got, want = _run(v, e, 3)
+    _same(got, want)
+    assert (got[2] == 0.0).all()
+
+
+@pytest.mark.parametrize("k", [4, 70])
+def test_random_multigraphs_vs_oracle(k):
+    rng = np.random.default_rng(k)
+    types = ["author", "paper", "venue", "topic"]
+    rels = ["author_of", "submit_at", "cites"]
+    for trial in range(25):
+        n = int(rng.integers(3, 90))
+        ty = rng.choice(types, size=n, p=[0.45, 0.35, 0.15, 0.05])
+        v = [(f"n{i}", f"L{i}", str(ty[i])) for i in range(n)]
+        m = int(rng.integers(0, 6 * n))
+        e = [(f"n{int(a)}", f"n{int(b)}", str(r)) for a, b, r in
+             zip(rng.integers(0, n, m), rng.integers(0, n, m), rng.choice(rels, size=m))]
+        res = _run(v, e, k)
+        if res is not None:
+            _same(*res)
+
+
+def test_row_slices_and_dequeue_order_do_not_change_results():
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_dblp
+    t = synth_dblp(6000, 18000, 300, seed=13).typed()
+    eng = build_engine(t, tile_w=1024)
+    full = [a.cpu().numpy() for a in eng.topk(10)]
+    plain = [a.cpu().numpy() for a in eng.topk(10, heavy_first=False)]
+    for a, b in zip(full, plain):
+        assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
+                              b.view(np.int64) if b.dtype == np.float64 else b)
+    for r0, r1 in ((0, 1), (17, 2000), (2000, 6000), (5999, 6000)):
+        part = [a.cpu().numpy() for a in eng.topk(10, r0, r1)]
+        for a, b in zip(part, full):
+            assert np.array_equal(a, b[r0:r1])
+
+
+def test_config3_full_output_properties():
+    import torch
+    from dpathsim import _lib
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_config
+    t = synth_config("config3").typed()
+    eng = build_engine(t)
+    k = 10
+    idx, cnt, sc = (a.cpu().numpy() for a in eng.topk(k))
+    na = t.n_authors
+    rows = np.arange(na)[:, None]
+    assert (idx >= 0).all() and (idx < na).all()            # every author has >= k targets
+    assert not (idx == rows).any()                           # self excluded
+    assert (np.diff(sc, axis=1) <= 0).all()                  # scores non-increasing
+    tie = np.diff(sc, axis=1) == 0
+    assert (np.diff(idx, axis=1)[tie] > 0).all()             # ties by ascending ordinal
+    srt = np.sort(idx, axis=1)
+    assert (np.diff(srt, axis=1) > 0).all()                  # distinct targets
+    assert (sc <= 1.0).all() and (cnt >= 0).all()
+    # sampled entries re-derived from the pairwise walk and the global walks
+    g = eng.tensor("g")[:na].cpu().numpy()
+    c_ptr = eng.tensor("c_ptr")
+    c_col, c_val = eng.tensor("c_col"), eng.tensor("c_val")
+    out = torch.empty(1, dtype=torch.int64, device=eng.device)
+    rng = np.random.default_rng(3)
+    for x, s in zip(rng.integers(0, na, 300), rng.integers(0, k, 300)):
+        y = int(idx[x, s])
+        a0, a1, b0, b1 = (int(u) for u in c_ptr[[x, x + 1, y, y + 1]].cpu())
+        _lib.call("dps_pair_count", c_col[a0:].data_ptr(), c_val[a0:].data_ptr(), a1 - a0,
+                  c_col[b0:].data_ptr(), c_val[b0:].data_ptr(), b1 - b0, out.data_ptr(),
+                  eng.stream)
+        m = int(out.item())
+        assert cnt[x, s] == m
+        want = np.float64(2 * m) / np.float64(int(g[x]) + int(g[y]))
+        assert sc[x, s].view(np.int64) == want.view(np.int64)
