@@ -162,6 +162,26 @@ def main():
             traffic = None
     info = eng.info
 
+    # ---- secondary rates the north star asks for -----------------------------
+    # SpGEMM (C = W_AP . W_PV) against HBM: SURVEY §8d algorithmic bytes over the
+    # 'spgemm' phase of one extra timed build (events on the stream; the phase
+    # includes the two host size reads of the two-pass SpGEMM).
+    eng.build(timed=True)
+    sp_ms = eng.info.phase_ms.get("spgemm", float("nan"))
+    sp_bytes = (16 * (NA + 1) + 8 * eng.info.nnz_ap + 4 * typed.n_papers + 8 * eng.info.nnz_c)
+    spgemm = {"bound": "hbm", "phase_ms": sp_ms, "algorithmic_bytes": sp_bytes,
+              "achieved": sp_bytes / (sp_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    spgemm["frac"] = spgemm["achieved"] / HBM_PEAK_GBS
+    # C.C^T against the dense int8 MFMA peak (5 POPS, MI355X_MICROARCH.md): the
+    # dense-equivalent rate (2 * rows * N_A * V padded to 64) and the intrinsic
+    # sparse rate (2 * sum_{x in shard} sum_{v in x} n_v multiply-adds).
+    v_pad = (typed.n_mids + 63) // 64 * 64
+    dense_ops = 2.0 * shard * NA * v_pad
+    cct = {"mfma_int8_dense_peak_ops": 5.0e15,
+           "dense_equiv_ops_per_s": dense_ops / (topk_ms * 1e-3),
+           "intrinsic_ops_per_s": 2.0 * terms / (topk_ms * 1e-3)}
+    cct["dense_equiv_frac_of_mfma_peak"] = cct["dense_equiv_ops_per_s"] / 5.0e15
+
     # ---- CPU baseline: the oracle's C port on a bounded row sample ----------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -215,6 +235,8 @@ def main():
                          "avg_launch_ms": topk_ms},
             "cpu_baseline": cpu,
             "phases_ms": {"cct_topk": topk_ms, "rest_of_step": ms_per_step - topk_ms},
+            "spgemm_roofline": spgemm,
+            "cct_vs_mfma": cct,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:
