@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--config", default="config3")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink authors/papers (debug)")
     ap.add_argument("--k", type=int, default=None)
-    ap.add_argument("--tile-w", type=int, default=32768)
+    ap.add_argument("--tile-w", type=int, default=8192)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01", "pmc_hot.json"),

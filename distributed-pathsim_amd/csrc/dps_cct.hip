@@ -48,8 +48,9 @@ constexpr bool kProfile = true;
 constexpr bool kProfile = false;
 #endif
 
-constexpr int kTB = 256;            // threads per workgroup
-constexpr int kNW = kTB / kWave;    // waves per workgroup
+// Waves per workgroup NW is a template parameter: 4 (256 threads) for tiles
+// up to W = 32768, 8 (512 threads) for W = 65536, so that a CU always holds 16
+// waves (4 workgroups x 32 KB or 2 x 64 KB of accumulators).
 constexpr int kU = 4;               // 16-B chunk loads in flight per lane
 constexpr int kQ = 2 * kWave;       // per-wave candidate queue (label, M) capacity
 
@@ -236,7 +237,7 @@ struct Stage {
   int64_t t;
   int lnp;       // log2(number of passes): 0 u8, 1 u16, 2 u32
   int pass;
-  int nb;        // batches of kTB*kU chunks (0 under the no-scatter ablation)
+  int nb;        // batches of NW*64*kU chunks (0 under the no-scatter ablation)
   int jc;        // venue cursor of issue(): venue of the last chunk block issued
   int64_t gq;    // lane s: smallest g of segment s of tile t
 };
@@ -246,7 +247,7 @@ struct Batch {
   int c[kU];
 };
 
-// Issue the loads of batch b of stage S: chunk q -> lane (q mod 256) of the
+// Issue the loads of batch b of stage S: chunk q -> lane (q mod 64*NW) of the
 // workgroup, kU chunks per lane.  Each load instruction reads 64 consecutive
 // chunks (q0 .. q0+63, q0 wave-uniform).  A wave-uniform venue cursor follows
 // the chunk blocks in order; when all 64 chunks of a load lie in the cursor's
@@ -254,12 +255,13 @@ struct Batch {
 // C[x,v] are scalars and the load costs a couple of VALU.  A load that straddles
 // venue boundaries resolves each lane's venue with chunk_venue().  Loads past
 // the stage's last chunk are skipped (uniform) and marked dead (c = 0).
+template <int NW>
 __device__ __forceinline__ void issue(Stage& S, int b, const uint32_t* __restrict__ ent,
                                       int wave, int lane, Batch& B, bool no_add,
                                       int p_ablate = 0, unsigned long long* p_counter = nullptr) {
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
-    const int q0 = b * (kTB * kU) + u * kTB + wave * kWave;   // wave-uniform
+    const int q0 = b * (NW * kWave * kU) + u * (NW * kWave) + wave * kWave;   // wave-uniform
     B.c[u] = 0;
     B.e[u] = make_uint4(0, 0, 0, 0);
     if (q0 >= S.G.nq) continue;
@@ -445,12 +447,12 @@ __device__ __forceinline__ uint32_t ge_u8(uint32_t a, uint32_t kA, uint32_t kB, 
 // has a bit at or above the highest power of two <= m; only then are its targets
 // compared exactly (SWAR) and the flagged ones appended to the wave's queue
 // lane-parallel (one round per candidate of the busiest lane).
-template <int KPL>
+template <int KPL, int NW>
 __device__ __forceinline__ void epilogue_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top,
                                             CandQ& Q, const Stage& S, int wave, int lane,
                                             int nbuf, int seg_shift, int64_t x_lab, int64_t gx,
                                             double tau_sh, int mseg) {
-  const int qd = nbuf / kNW;
+  const int qd = nbuf / NW;
   const int end = (wave + 1) * qd;
   const int64_t tile_base = S.t << p.shift;
   const bool score = (p.ablate & 2) == 0;
@@ -521,16 +523,16 @@ __device__ __forceinline__ int stage_mseg(const TopK<KPL>& top, const Stage& S, 
   return mseg;
 }
 
-template <int KPL>
+template <int KPL, int NW>
 __device__ __forceinline__ void epilogue(const CctParams& p, uint32_t* acc, TopK<KPL>& top,
                                          CandQ& Q, const Stage& S, int wave, int lane, int nbuf,
                                          int seg_shift, int64_t x_lab, int64_t gx,
                                          double tau_sh, int mseg) {
   if (S.lnp == 0) {
-    epilogue_u8<KPL>(p, acc, top, Q, S, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh, mseg);
+    epilogue_u8<KPL, NW>(p, acc, top, Q, S, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh, mseg);
     return;
   }
-  const int qd = nbuf / kNW;
+  const int qd = nbuf / NW;
   const int end = (wave + 1) * qd;
   const int lnp = S.lnp;
   const int tpd_shift = 2 - lnp;                     // log2(targets per dword)
@@ -585,6 +587,7 @@ struct Window {
 // window's loads for the following tile are issued as soon as the current
 // tile's values are consumed, so on a taken stage they complete behind the
 // scatter and epilogue.
+template <int NW>
 __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d, int lane,
                                            int64_t gx, double tau_sh, int seg_shift,
                                            bool no_scatter, Stage& S) {
@@ -615,7 +618,7 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
     S.jc = 0;
     grp_set(S.G, lo, hi, w.c, d);
     if (no_scatter) S.G.nq = 0;
-    S.nb = (S.G.nq + kTB * kU - 1) / (kTB * kU);
+    S.nb = (S.G.nq + NW * kWave * kU - 1) / (NW * kWave * kU);
     S.gq = p.g_t[min((t << p.shift) + (static_cast<int64_t>(lane) << seg_shift),
                      p.n_targets - 1)];
     return true;
@@ -626,15 +629,15 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
   return false;
 }
 
-template <int KPL>
-__global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k_cct_topk(CctParams p, int acc_dw) {
+template <int KPL, int NW>
+__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_cct_topk(CctParams p, int acc_dw) {
   // All LDS is dynamic, so the accumulators start at LDS address 0 and each
   // stage buffer is W-byte aligned (scatter_u8 ORs the in-tile offset in).
   // Layout: [2 stage buffers | per-wave queues | tau_s | fill_s | row_s].
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  double (*tau_s)[kNW] = reinterpret_cast<double (*)[kNW]>(lds + acc_dw + kNW * 2 * kQ);
-  int* fill_s = reinterpret_cast<int*>(lds + acc_dw + kNW * 2 * kQ + 4 * kNW);
-  long long& row_s = *reinterpret_cast<long long*>(lds + acc_dw + kNW * 2 * kQ + 5 * kNW);
+  double (*tau_s)[NW] = reinterpret_cast<double (*)[NW]>(lds + acc_dw + NW * 2 * kQ);
+  int* fill_s = reinterpret_cast<int*>(lds + acc_dw + NW * 2 * kQ + 4 * NW);
+  long long& row_s = *reinterpret_cast<long long*>(lds + acc_dw + NW * 2 * kQ + 5 * NW);
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_u32*)lds));
   const uint32_t lab_mask = ((1u << p.shift) - 1u) & ~3u;
   const int tid = threadIdx.x;
@@ -649,7 +652,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
   Q.lab = reinterpret_cast<int*>(lds + acc_dw) + wave * 2 * kQ;
   Q.m = Q.lab + kQ;
   Q.n = 0;
-  for (int i = tid; i < acc_dw; i += kTB) lds[i] = 0;
+  for (int i = tid; i < acc_dw; i += NW * kWave) lds[i] = 0;
 
   for (;;) {
     if (tid == 0) row_s = static_cast<long long>(atomicAdd(p.counter, 1ull));
@@ -686,14 +689,14 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         w.mx = p.tile_maxc[vb];
       }
       Stage cur;
-      bool have = find_stage(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, cur);
+      bool have = find_stage<NW>(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, cur);
       // Batch 0 of the current stage is loaded one epilogue ahead.  It is issued
       // unconditionally (a missing stage loads dead chunks with C = 0) so B has
       // one definition in the loop and the register allocator need not copy it
       // -- a copy would wait on the loads at once and expose their latency.
       Batch B;
       if (!have) cur.G.nq = 0;
-      issue(cur, 0, p.tile_ent, wave, lane, B, no_add, p.ablate, p.counter);
+      issue<NW>(cur, 0, p.tile_ent, wave, lane, B, no_add, p.ablate, p.counter);
       // profiling aid (DPATHSIM_ABLATE & 16): shader-clock cycles per phase
       const bool prof = kProfile && (p.ablate & 16) != 0;
       uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pc[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -705,7 +708,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         scatter_any(B, cur, acc, buf, lab_mask, p.shift);
         for (int b = 1; b < cur.nb; ++b) {
           Batch B2;
-          issue(cur, b, p.tile_ent, wave, lane, B2, no_add, p.ablate, p.counter);
+          issue<NW>(cur, b, p.tile_ent, wave, lane, B2, no_add, p.ablate, p.counter);
           scatter_any(B2, cur, acc, buf, lab_mask, p.shift);
         }
         if (prof) ts[1] = __builtin_amdgcn_s_memtime();
@@ -720,7 +723,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         if (prof) ts[3] = __builtin_amdgcn_s_memtime();
         double tm = tau_s[n & 1][0];
 #pragma unroll
-        for (int i = 1; i < kNW; ++i) tm = tau_s[n & 1][i] > tm ? tau_s[n & 1][i] : tm;
+        for (int i = 1; i < NW; ++i) tm = tau_s[n & 1][i] > tm ? tau_s[n & 1][i] : tm;
         tau_sh = tm;
         const int mseg = stage_mseg(top, cur, gx, tau_sh);
         // find the next stage and put its first loads in flight before this
@@ -728,12 +731,12 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
         Stage nxt;
         bool have_n;
         if (cur.pass + 1 < (1 << cur.lnp)) { nxt = cur; ++nxt.pass; nxt.jc = 0; have_n = true; }
-        else have_n = find_stage(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, nxt);
+        else have_n = find_stage<NW>(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, nxt);
         if (!have_n) nxt.G.nq = 0;
         if (prof) ts[4] = __builtin_amdgcn_s_memtime();
-        issue(nxt, 0, p.tile_ent, wave, lane, B, no_add, p.ablate, p.counter);
+        issue<NW>(nxt, 0, p.tile_ent, wave, lane, B, no_add, p.ablate, p.counter);
         if (prof) ts[5] = __builtin_amdgcn_s_memtime();
-        epilogue<KPL>(p, acc, top, Q, cur, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh, mseg);
+        epilogue<KPL, NW>(p, acc, top, Q, cur, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh, mseg);
         if (prof) ts[6] = __builtin_amdgcn_s_memtime();
         if (!p.dbuf) __syncthreads();   // one buffer: every wave has zeroed its quarter
         if (prof) {
@@ -785,10 +788,10 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
             }
             grp_set(S.G, lo, hi, c, d - g0 < kWave ? d - g0 : kWave);
             S.jc = 0;
-            S.nb = (S.G.nq + kTB * kU - 1) / (kTB * kU);
+            S.nb = (S.G.nq + NW * kWave * kU - 1) / (NW * kWave * kU);
             for (int b = 0; b < S.nb; ++b) {
               Batch B;
-              issue(S, b, p.tile_ent, wave, lane, B, no_add);
+              issue<NW>(S, b, p.tile_ent, wave, lane, B, no_add);
               scatter_any(B, S, acc, buf, lab_mask, p.shift);
             }
           }
@@ -798,9 +801,9 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
           __syncthreads();
           double tm = tau_s[n & 1][0];
 #pragma unroll
-          for (int i = 1; i < kNW; ++i) tm = tau_s[n & 1][i] > tm ? tau_s[n & 1][i] : tm;
+          for (int i = 1; i < NW; ++i) tm = tau_s[n & 1][i] > tm ? tau_s[n & 1][i] : tm;
           tau_sh = tm;
-          epilogue<KPL>(p, acc, top, Q, S, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh,
+          epilogue<KPL, NW>(p, acc, top, Q, S, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh,
                         stage_mseg(top, S, gx, tau_sh));
           if (!p.dbuf) __syncthreads();
           ++n;
@@ -811,9 +814,9 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     __syncthreads();   // every wave has finished scanning (and zeroing) its last stage
 
     // ---- merge the four wave lists (the accumulators are all zero; reuse) ---
-    double* ms = reinterpret_cast<double*>(lds);          // [kNW][k]
-    int* my = reinterpret_cast<int*>(ms + kNW * p.k);     // [kNW][k]
-    int* mm = my + kNW * p.k;                              // [kNW][k]
+    double* ms = reinterpret_cast<double*>(lds);          // [NW][k]
+    int* my = reinterpret_cast<int*>(ms + NW * p.k);     // [NW][k]
+    int* mm = my + NW * p.k;                              // [NW][k]
 #pragma unroll
     for (int q = 0; q < KPL; ++q) {
       const int slot = q * kWave + lane;
@@ -826,7 +829,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
     if (lane == 0) fill_s[wave] = top.filled;
     __syncthreads();
     if (wave == 0) {
-      for (int w = 1; w < kNW; ++w) {
+      for (int w = 1; w < NW; ++w) {
         const int nf = fill_s[w];
         for (int i = 0; i < nf; ++i) {
           const double cs = ms[w * p.k + i];
@@ -872,7 +875,7 @@ __global__ __launch_bounds__(kTB) __attribute__((amdgpu_waves_per_eu(4))) void k
       }
     }
     __syncthreads();
-    for (int i = tid; i < kNW * p.k * 4; i += kTB) lds[i] = 0;   // 16 B per merge entry
+    for (int i = tid; i < NW * p.k * 4; i += NW * kWave) lds[i] = 0;   // 16 B per merge entry
   }
 }
 
@@ -882,15 +885,15 @@ int log2_exact(int32_t w) {
   return (1 << s) == w ? s : -1;
 }
 
-template <int KPL>
+template <int KPL, int NW>
 int launch(const CctParams& p, hipStream_t st) {
   // one or two stage buffers of W/4 dwords; the row-end merge reuses them (16 B
   // per entry)
   int acc_dw = (p.dbuf ? 2 : 1) * (1 << (p.shift - 2));
-  if (acc_dw < 4 * kNW * p.k) acc_dw = 4 * kNW * p.k;
-  // + tau_s (2*kNW doubles) + fill_s (kNW ints) + row_s (one 8-byte slot)
-  const size_t lds = (static_cast<size_t>(acc_dw) + kNW * 2 * kQ + 5 * kNW + 2) * sizeof(uint32_t);
-  DPS_HIP_RET(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cct_topk<KPL>),
+  if (acc_dw < 4 * NW * p.k) acc_dw = 4 * NW * p.k;
+  // + tau_s (2*NW doubles) + fill_s (NW ints) + row_s (one 8-byte slot)
+  const size_t lds = (static_cast<size_t>(acc_dw) + NW * 2 * kQ + 5 * NW + 2) * sizeof(uint32_t);
+  DPS_HIP_RET(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cct_topk<KPL, NW>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   static_cast<int>(lds)));
   int dev = 0, n_cu = 256;
@@ -898,10 +901,10 @@ int launch(const CctParams& p, hipStream_t st) {
   DPS_HIP_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
   int per_cu = static_cast<int>((160 * 1024) / (lds + 256));
   if (per_cu < 1) per_cu = 1;
-  if (per_cu > 8) per_cu = 8;   // 32 waves per CU
+  if (per_cu > 16 / NW) per_cu = 16 / NW;   // 4 waves per SIMD (128 VGPRs each)
   int64_t grid = static_cast<int64_t>(n_cu) * per_cu;
   if (grid > p.n_rows) grid = p.n_rows;
-  k_cct_topk<KPL><<<static_cast<unsigned>(grid), kTB, lds, st>>>(p, acc_dw);
+  k_cct_topk<KPL, NW><<<static_cast<unsigned>(grid), NW * kWave, lds, st>>>(p, acc_dw);
   DPS_LAUNCHED();
   return DPS_OK;
 }
@@ -950,16 +953,32 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   p.n_targets = n_targets;
   p.T = (n_targets + tile_w - 1) / tile_w;
   p.shift = shift;
-  p.dbuf = shift <= 14;   // 2 x W bytes of u8 accumulators up to W = 16384, one 32 KB buffer above
+  // waves per row: one wave owns a row for W <= 8192 (8 KB of u8 accumulators,
+  // no barriers, one exact running top-k per row); wider tiles share a row
+  // between the waves of a workgroup (4 x 32 KB or 2 x 64 KB per CU)
+  int nw = shift <= 13 ? 1 : shift == 16 ? 8 : 4;
+  if (const char* e = std::getenv("DPATHSIM_NW")) nw = std::atoi(e);
+  DPS_REQUIRE(nw == 1 || nw == 4 || nw == 8, DPS_ERR_INVALID, "DPATHSIM_NW must be 1, 4 or 8");
+  p.dbuf = nw > 1 && shift <= 14;   // 2 x W bytes of u8 accumulators up to W = 16384, one 32 KB buffer above
   p.row_begin = row_begin; p.row_order = row_order; p.n_rows = n_rows; p.k = k;
   p.out_idx = out_idx; p.out_cnt = out_cnt; p.out_score = out_score;
   p.counter = static_cast<unsigned long long*>(ws);
   p.ablate = 0;
   if (const char* ab = std::getenv("DPATHSIM_ABLATE")) p.ablate = std::atoi(ab);
   DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : sizeof(unsigned long long), st));
-  if (k <= 64) return launch<1>(p, st);
-  if (k <= 128) return launch<2>(p, st);
-  return launch<4>(p, st);
+  if (nw == 8) {   // 64 KB of u8 accumulators: 8-wave workgroups, two per CU
+    if (k <= 64) return launch<1, 8>(p, st);
+    if (k <= 128) return launch<2, 8>(p, st);
+    return launch<4, 8>(p, st);
+  }
+  if (nw == 1) {   // one wave per row
+    if (k <= 64) return launch<1, 1>(p, st);
+    if (k <= 128) return launch<2, 1>(p, st);
+    return launch<4, 1>(p, st);
+  }
+  if (k <= 64) return launch<1, 4>(p, st);
+  if (k <= 128) return launch<2, 4>(p, st);
+  return launch<4, 4>(p, st);
 }
 
 }  // extern "C"

@@ -16,7 +16,7 @@ import torch
 from . import _lib
 from .graph import TypedTables
 
-DEFAULT_TILE_W = 32768
+DEFAULT_TILE_W = 8192
 
 
 def _ptr(t):

@@ -23,7 +23,7 @@ def _check(eng, co, k, rows=None):
                            f"orc {oi[bad[0]]} {oc[bad[0]]} {os_[bad[0]]}")
 
 
-@pytest.mark.parametrize("tile_w", [256, 1024, 4096, 32768, 65536])
+@pytest.mark.parametrize("tile_w", [256, 1024, 4096, 8192, 32768, 65536])
 def test_synth_20k_top10(tile_w):
     from dpathsim.engine import build_engine
     from dpathsim.synth import synth_dblp
@@ -38,6 +38,18 @@ def test_synth_20k_top10(tile_w):
     assert np.array_equal(eng.tensor("c_val")[:nnz].cpu().numpy(), cv)
     assert np.array_equal(eng.tensor("g")[: t.n_authors].cpu().numpy(), gg)
     _check(eng, co, 10)
+
+
+@pytest.mark.parametrize("tile_w,nw", [(8192, 1), (8192, 4), (4096, 4), (16384, 1), (32768, 1)])
+def test_synth_20k_waves_per_row(tile_w, nw, monkeypatch):
+    """Both kernel shapes -- one wave per row and a workgroup per row
+    (DPATHSIM_NW overrides the tile-width default) -- give the oracle's top-k."""
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_dblp
+    monkeypatch.setenv("DPATHSIM_NW", str(nw))
+    t = synth_dblp(20_000, 60_000, 500, seed=7).typed()
+    _check(build_engine(t, tile_w=tile_w), _oracle(t), 10)
+    _check(build_engine(t, tile_w=tile_w), _oracle(t), 100, rows=(0, 3000))
 
 
 @pytest.mark.parametrize("k", [1, 64, 65, 100, 200, 256])

@@ -1,0 +1,40 @@
+"""Hot-kernel A/B across tile widths and waves per row on a config (all rows by
+default): times eng.topk for each (W, NW) and checks the outputs are
+bit-identical to the first run's."""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "distributed-pathsim_amd"))
+import numpy as np
+import torch
+from dpathsim.synth import synth_config, CONFIGS
+from dpathsim.engine import build_engine
+
+cfg = os.environ.get("AB_CONFIG", "config3")
+K = int(os.environ.get("AB_K", str(CONFIGS[cfg][4])))
+# cases "W:NW" (tile width : waves per workgroup, DPATHSIM_NW)
+cases = [tuple(int(v) for v in c.split(":")) for c in os.environ.get("AB_CASES", "32768:4,8192:1").split(",")]
+import dpathsim
+t = synth_config(cfg).typed(dpathsim.METAPATHS[CONFIGS[cfg][3]])
+R = int(os.environ.get("AB_ROWS", str(t.n_authors)))
+ref = None
+eng, W0 = None, None
+for W, NW in cases:
+    if W != W0:
+        eng = None
+        torch.cuda.empty_cache()
+        eng, W0 = build_engine(t, tile_w=W), W
+    os.environ["DPATHSIM_NW"] = str(NW)
+    eng.topk(K, 0, min(R, 20000)); torch.cuda.synchronize()
+    if True:
+        best = 1e30
+        for _ in range(int(os.environ.get("AB_REPS", "2"))):
+            e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(); o = eng.topk(K, 0, R); e1.record(); torch.cuda.synchronize()
+            best = min(best, e0.elapsed_time(e1))
+        o = [a.cpu().numpy() for a in o]
+        print(f"{cfg} W={W} NW={NW}: {best:.1f} ms for {R} rows (k={K})", flush=True)
+        if ref is None:
+            ref = o
+        else:
+            bad = np.flatnonzero((o[0] != ref[0]).any(1) | (o[1] != ref[1]).any(1) |
+                                 (o[2].view(np.int64) != ref[2].view(np.int64)).any(1))
+            print(f"  vs first: {len(bad)} rows differ {bad[:5].tolist()}", flush=True)
