@@ -52,6 +52,10 @@ constexpr bool kProfile = false;
 // up to W = 32768, 8 (512 threads) for W = 65536, so that a CU always holds 16
 // waves (4 workgroups x 32 KB or 2 x 64 KB of accumulators).
 constexpr int kU = 4;               // 16-B chunk loads in flight per lane
+#ifndef DPS_EPIU
+#define DPS_EPIU 4
+#endif
+constexpr int kEpiU = DPS_EPIU;    // epilogue blocks read per trip
 constexpr int kQ = 2 * kWave;       // per-wave candidate queue (label, M) capacity
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -458,19 +462,15 @@ __device__ __forceinline__ void epilogue_u8(const CctParams& p, uint32_t* acc, T
   const bool score = (p.ablate & 2) == 0;
   const int64_t xr64 = x_lab - tile_base;
   const int xrel = (xr64 >= 0 && xr64 < (int64_t(1) << p.shift)) ? static_cast<int>(xr64) : -64;
-  for (int b0 = wave * qd; b0 < end; b0 += kWave * 4) {
+  // one iteration: the 16-byte block of each lane (1024 targets, one segment)
+  auto block = [&](uint4 a, int b0) {
     const int b = b0 + lane * 4;
-    uint4 a = make_uint4(0, 0, 0, 0);
-    if (b < end) {
-      a = *reinterpret_cast<const uint4*>(acc + b);
-      *reinterpret_cast<uint4*>(acc + b) = make_uint4(0, 0, 0, 0);
-    }
     const uint32_t m = static_cast<uint32_t>(readlane(mseg, (b0 << 2) >> seg_shift));
-    if (m > 255u || !score) continue;                          // no u8 count reaches m
+    if (m > 255u || !score) return;                          // no u8 count reaches m
     const uint32_t pm = (0x100u - (0x80000000u >> __builtin_clz(m))) * 0x01010101u;
     const uint32_t any = (a.x | a.y | a.z | a.w) & pm;
     if ((kProfile && (p.ablate & 8)) && lane == 0) atomicAdd(p.counter + 16, 1ull);   // iterations scanned
-    if (!ballot(any != 0)) continue;
+    if (!ballot(any != 0)) return;
     if ((kProfile && (p.ablate & 8)) && lane == 0) atomicAdd(p.counter + 17, 1ull);   // prefilter passes
     const uint32_t kA = __builtin_amdgcn_perm(0u, 128u - m, 0u);   // byte 0 broadcast
     const uint32_t kB = __builtin_amdgcn_perm(0u, 256u - m, 0u);
@@ -481,7 +481,7 @@ __device__ __forceinline__ void epilogue_u8(const CctParams& p, uint32_t* acc, T
     const int i0 = b << 2;                                     // first target of the block
     const int rel = xrel - i0;                                 // the source itself never counts
     if (rel >= 0 && rel < 16) F &= ~(1u << ((rel & 3) * 8 + 7 - (rel >> 2)));
-    if (!ballot(F != 0)) continue;
+    if (!ballot(F != 0)) return;
     if ((kProfile && (p.ablate & 8)) && lane == 0) atomicAdd(p.counter + 18, 1ull);   // exact passes
     wave_lds_fence();
     for (;;) {
@@ -503,6 +503,31 @@ __device__ __forceinline__ void epilogue_u8(const CctParams& p, uint32_t* acc, T
       Q.n += __popcll(mk);
       if (Q.n >= kWave) flush<KPL>(p, Q, top, kWave, gx, tau_sh, lane);
     }
+  };
+  if (qd % (kWave * 4 * kEpiU) == 0) {
+    // whole iterations, kEpiU per trip: all blocks are read (and zeroed) before
+    // any is judged, so one LDS latency covers kEpiU segments
+    for (int b0 = wave * qd; b0 < end; b0 += kWave * 4 * kEpiU) {
+      const int b = b0 + lane * 4;
+      uint4 a[kEpiU];
+#pragma unroll
+      for (int i = 0; i < kEpiU; ++i) a[i] = *reinterpret_cast<const uint4*>(acc + b + i * kWave * 4);
+#pragma unroll
+      for (int i = 0; i < kEpiU; ++i)
+        *reinterpret_cast<uint4*>(acc + b + i * kWave * 4) = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < kEpiU; ++i) block(a[i], b0 + i * kWave * 4);
+    }
+    return;
+  }
+  for (int b0 = wave * qd; b0 < end; b0 += kWave * 4) {
+    const int b = b0 + lane * 4;
+    uint4 a = make_uint4(0, 0, 0, 0);
+    if (b < end) {
+      a = *reinterpret_cast<const uint4*>(acc + b);
+      *reinterpret_cast<uint4*>(acc + b) = make_uint4(0, 0, 0, 0);
+    }
+    block(a, b0);
   }
 }
 
@@ -717,6 +742,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         // no prefetch is in flight, so its loads do not wait on the prefetch
         if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
           flush<KPL>(p, Q, top, Q.n, gx, tau_sh, lane);
+        // (one-wave rows too: skipping this LDS round trip measured 7 % slower)
         if (lane == 0) tau_s[n & 1][wave] = top.full() ? top.kth_s : -1.0;
         if (prof) ts[2] = __builtin_amdgcn_s_memtime();
         __syncthreads();
@@ -813,21 +839,23 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
     if (Q.n > 0) flush<KPL>(p, Q, top, Q.n, gx, tau_sh, lane);
     __syncthreads();   // every wave has finished scanning (and zeroing) its last stage
 
-    // ---- merge the four wave lists (the accumulators are all zero; reuse) ---
+    // ---- merge the wave lists (the accumulators are all zero; reuse) ---
     double* ms = reinterpret_cast<double*>(lds);          // [NW][k]
     int* my = reinterpret_cast<int*>(ms + NW * p.k);     // [NW][k]
     int* mm = my + NW * p.k;                              // [NW][k]
+    if constexpr (NW > 1) {   // one-wave rows write straight from registers
 #pragma unroll
-    for (int q = 0; q < KPL; ++q) {
-      const int slot = q * kWave + lane;
-      if (slot < top.filled) {
-        ms[wave * p.k + slot] = top.s[q];
-        my[wave * p.k + slot] = top.y[q];
-        mm[wave * p.k + slot] = top.m[q];
+      for (int q = 0; q < KPL; ++q) {
+        const int slot = q * kWave + lane;
+        if (slot < top.filled) {
+          ms[wave * p.k + slot] = top.s[q];
+          my[wave * p.k + slot] = top.y[q];
+          mm[wave * p.k + slot] = top.m[q];
+        }
       }
+      if (lane == 0) fill_s[wave] = top.filled;
+      __syncthreads();
     }
-    if (lane == 0) fill_s[wave] = top.filled;
-    __syncthreads();
     if (wave == 0) {
       for (int w = 1; w < NW; ++w) {
         const int nf = fill_s[w];
@@ -874,8 +902,10 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         os[s2] = 0.0;
       }
     }
-    __syncthreads();
-    for (int i = tid; i < NW * p.k * 4; i += NW * kWave) lds[i] = 0;   // 16 B per merge entry
+    if constexpr (NW > 1) {
+      __syncthreads();
+      for (int i = tid; i < NW * p.k * 4; i += NW * kWave) lds[i] = 0;   // 16 B per merge entry
+    }
   }
 }
 

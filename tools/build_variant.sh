@@ -1,0 +1,12 @@
+#!/bin/bash
+# Build ab/libdpathsim_<name>.so: dps_cct.hip compiled with extra flags ($2...),
+# linked with the other objects of the regular build (run `make` first).
+set -eu
+cd "$(dirname "$0")/../distributed-pathsim_amd/csrc"
+name=$1; shift
+mkdir -p ../../ab
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -Wall -Wno-unused-function \
+  -munsafe-fp-atomics "$@" -c dps_cct.hip -o /tmp/cct_$name.o
+objs=$(ls build/*.o | grep -v dps_cct | grep -v dps_topk)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../ab/libdpathsim_$name.so /tmp/cct_$name.o $objs
+echo built ab/libdpathsim_$name.so

@@ -34,7 +34,7 @@ write = per_dispatch(sys.argv[2], "WRITE_SIZE")
 f_kib = sum(fetch) / len(fetch)
 w_kib = sum(write) / len(write)
 rec = {"kernel": "k_cct_topk", "config": "config3", "world": 1,
-       "tile_w": int(sys.argv[4]) if len(sys.argv) > 4 else 32768,
+       "tile_w": int(sys.argv[4]) if len(sys.argv) > 4 else 8192,
        "fetch_size_kib": f_kib, "write_size_kib": w_kib,
        "hbm_bytes_per_launch": 2 * f_kib * 1024 + w_kib * 1024,
        "rule": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950: FETCH_SIZE = half of 16-B/lane reads)",
