@@ -295,10 +295,10 @@ __device__ __forceinline__ void issue(Stage& S, int b, const uint32_t* __restric
   }
 }
 
-__device__ __forceinline__ void acc_add(uint32_t* acc, uint32_t e, int c, int lnp, int pass,
-                                        int shift) {
-  const uint32_t yl = e & 0xFFFFu;
-  const uint32_t val = static_cast<uint32_t>(c) * (e >> 16);
+// One entry (tile-local label yl, count ce) into the u16 / u32 accumulators.
+__device__ __forceinline__ void acc_add(uint32_t* acc, uint32_t yl, uint32_t ce, int c, int lnp,
+                                        int pass, int shift) {
+  const uint32_t val = static_cast<uint32_t>(c) * ce;
   if (val == 0) return;
   uint32_t* dst;
   uint32_t add;
@@ -319,14 +319,28 @@ __device__ __forceinline__ void acc_add(uint32_t* acc, uint32_t e, int c, int ln
   __hip_atomic_fetch_add(dst, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// A word of entries: two 16-bit entries (c << 13 | label) when P16, else one
+// 32-bit entry (C << 16 | label).
+template <bool P16>
+__device__ __forceinline__ void acc_add_word(uint32_t* acc, uint32_t w, int c, int lnp, int pass,
+                                             int shift) {
+  if constexpr (P16) {
+    acc_add(acc, w & 0x1FFFu, (w >> 13) & 7u, c, lnp, pass, shift);
+    acc_add(acc, (w >> 16) & 0x1FFFu, w >> 29, c, lnp, pass, shift);
+  } else {
+    acc_add(acc, w & 0xFFFFu, w >> 16, c, lnp, pass, shift);
+  }
+}
+
+template <bool P16>
 __device__ __forceinline__ void scatter(const Batch& B, const Stage& S, uint32_t* acc, int shift) {
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     if (B.c[u] == 0) continue;
-    acc_add(acc, B.e[u].x, B.c[u], S.lnp, S.pass, shift);
-    acc_add(acc, B.e[u].y, B.c[u], S.lnp, S.pass, shift);
-    acc_add(acc, B.e[u].z, B.c[u], S.lnp, S.pass, shift);
-    acc_add(acc, B.e[u].w, B.c[u], S.lnp, S.pass, shift);
+    acc_add_word<P16>(acc, B.e[u].x, B.c[u], S.lnp, S.pass, shift);
+    acc_add_word<P16>(acc, B.e[u].y, B.c[u], S.lnp, S.pass, shift);
+    acc_add_word<P16>(acc, B.e[u].z, B.c[u], S.lnp, S.pass, shift);
+    acc_add_word<P16>(acc, B.e[u].w, B.c[u], S.lnp, S.pass, shift);
   }
 }
 
@@ -344,22 +358,44 @@ __device__ __forceinline__ void add_u8(uint32_t buf, uint32_t e, uint32_t c, uin
                          add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// The same for a word of two 16-bit entries (c << 13) | label (W <= 8192): the
+// low entry's byte shift is (w << 3) mod 32, the high one's (w >> 13) & 24.
+__device__ __forceinline__ void add_u8_p16(uint32_t buf, uint32_t w, uint32_t c,
+                                           uint32_t lab_mask) {
+  const uint32_t alo = __umul24(c, (w >> 13) & 7u) << ((w << 3) & 24u);
+  const uint32_t ahi = __umul24(c, w >> 29) << ((w >> 13) & 24u);
+  __hip_atomic_fetch_add(reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(buf | (w & lab_mask))),
+                         alo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_add(
+      reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(buf | ((w >> 16) & lab_mask))), ahi,
+      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <bool P16>
+__device__ __forceinline__ void add_u8_word(uint32_t buf, uint32_t w, uint32_t c,
+                                            uint32_t lab_mask) {
+  if constexpr (P16) add_u8_p16(buf, w, c, lab_mask);
+  else add_u8(buf, w, c, lab_mask);
+}
+
+template <bool P16>
 __device__ __forceinline__ void scatter_u8(const Batch& B, uint32_t buf, uint32_t lab_mask) {
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const uint32_t c = static_cast<uint32_t>(B.c[u]);
     if (c == 0) continue;   // dead chunk (beyond the stage's last)
-    add_u8(buf, B.e[u].x, c, lab_mask);
-    add_u8(buf, B.e[u].y, c, lab_mask);
-    add_u8(buf, B.e[u].z, c, lab_mask);
-    add_u8(buf, B.e[u].w, c, lab_mask);
+    add_u8_word<P16>(buf, B.e[u].x, c, lab_mask);
+    add_u8_word<P16>(buf, B.e[u].y, c, lab_mask);
+    add_u8_word<P16>(buf, B.e[u].z, c, lab_mask);
+    add_u8_word<P16>(buf, B.e[u].w, c, lab_mask);
   }
 }
 
+template <bool P16>
 __device__ __forceinline__ void scatter_any(const Batch& B, const Stage& S, uint32_t* acc,
                                             uint32_t buf, uint32_t lab_mask, int shift) {
-  if (S.lnp == 0) scatter_u8(B, buf, lab_mask);
-  else scatter(B, S, acc, shift);
+  if (S.lnp == 0) scatter_u8<P16>(B, buf, lab_mask);
+  else scatter<P16>(B, S, acc, shift);
 }
 
 __device__ __forceinline__ void wave_lds_fence() {
@@ -654,7 +690,9 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
   return false;
 }
 
-template <int KPL, int NW>
+// Entry format of the tiles (dps_ct_tiles_build): P16 = 16-bit entries
+// (W <= 8192), else 32-bit entries.
+template <int KPL, int NW, bool P16>
 __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_cct_topk(CctParams p, int acc_dw) {
   // All LDS is dynamic, so the accumulators start at LDS address 0 and each
   // stage buffer is W-byte aligned (scatter_u8 ORs the in-tile offset in).
@@ -730,11 +768,11 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         const int bi = p.dbuf ? (n & 1) : 0;
         uint32_t* acc = lds + bi * nbuf;
         const uint32_t buf = lds0 + static_cast<uint32_t>(bi * nbuf) * 4u;
-        scatter_any(B, cur, acc, buf, lab_mask, p.shift);
+        scatter_any<P16>(B, cur, acc, buf, lab_mask, p.shift);
         for (int b = 1; b < cur.nb; ++b) {
           Batch B2;
           issue<NW>(cur, b, p.tile_ent, wave, lane, B2, no_add, p.ablate, p.counter);
-          scatter_any(B2, cur, acc, buf, lab_mask, p.shift);
+          scatter_any<P16>(B2, cur, acc, buf, lab_mask, p.shift);
         }
         if (prof) ts[1] = __builtin_amdgcn_s_memtime();
         // score what is queued while the wave's list is filling or the queue is
@@ -818,7 +856,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
             for (int b = 0; b < S.nb; ++b) {
               Batch B;
               issue<NW>(S, b, p.tile_ent, wave, lane, B, no_add);
-              scatter_any(B, S, acc, buf, lab_mask, p.shift);
+              scatter_any<P16>(B, S, acc, buf, lab_mask, p.shift);
             }
           }
           if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
@@ -915,7 +953,7 @@ int log2_exact(int32_t w) {
   return (1 << s) == w ? s : -1;
 }
 
-template <int KPL, int NW>
+template <int KPL, int NW, bool P16>
 int launch(const CctParams& p, hipStream_t st) {
   // one or two stage buffers of W/4 dwords; the row-end merge reuses them (16 B
   // per entry)
@@ -923,7 +961,7 @@ int launch(const CctParams& p, hipStream_t st) {
   if (acc_dw < 4 * NW * p.k) acc_dw = 4 * NW * p.k;
   // + tau_s (2*NW doubles) + fill_s (NW ints) + row_s (one 8-byte slot)
   const size_t lds = (static_cast<size_t>(acc_dw) + NW * 2 * kQ + 5 * NW + 2) * sizeof(uint32_t);
-  DPS_HIP_RET(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cct_topk<KPL, NW>),
+  DPS_HIP_RET(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cct_topk<KPL, NW, P16>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   static_cast<int>(lds)));
   int dev = 0, n_cu = 256;
@@ -934,9 +972,30 @@ int launch(const CctParams& p, hipStream_t st) {
   if (per_cu > 16 / NW) per_cu = 16 / NW;   // 4 waves per SIMD (128 VGPRs each)
   int64_t grid = static_cast<int64_t>(n_cu) * per_cu;
   if (grid > p.n_rows) grid = p.n_rows;
-  k_cct_topk<KPL, NW><<<static_cast<unsigned>(grid), NW * kWave, lds, st>>>(p, acc_dw);
+  k_cct_topk<KPL, NW, P16><<<static_cast<unsigned>(grid), NW * kWave, lds, st>>>(p, acc_dw);
   DPS_LAUNCHED();
   return DPS_OK;
+}
+
+template <bool P16>
+int dispatch(const CctParams& p, int nw, int k, hipStream_t st) {
+  if (nw == 8) {   // 64 KB of u8 accumulators: 8-wave workgroups, two per CU
+    if constexpr (P16) {
+      return DPS_ERR_INVALID;   // never: 8 waves only for W = 65536
+    } else {
+      if (k <= 64) return launch<1, 8, P16>(p, st);
+      if (k <= 128) return launch<2, 8, P16>(p, st);
+      return launch<4, 8, P16>(p, st);
+    }
+  }
+  if (nw == 1) {   // one wave per row
+    if (k <= 64) return launch<1, 1, P16>(p, st);
+    if (k <= 128) return launch<2, 1, P16>(p, st);
+    return launch<4, 1, P16>(p, st);
+  }
+  if (k <= 64) return launch<1, 4, P16>(p, st);
+  if (k <= 128) return launch<2, 4, P16>(p, st);
+  return launch<4, 4, P16>(p, st);
 }
 
 }  // namespace
@@ -989,6 +1048,8 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   int nw = shift <= 13 ? 1 : shift == 16 ? 8 : 4;
   if (const char* e = std::getenv("DPATHSIM_NW")) nw = std::atoi(e);
   DPS_REQUIRE(nw == 1 || nw == 4 || nw == 8, DPS_ERR_INVALID, "DPATHSIM_NW must be 1, 4 or 8");
+  DPS_REQUIRE(nw != 8 || shift > 13, DPS_ERR_INVALID, "8 waves per row need tile_w >= 16384");
+
   p.dbuf = nw > 1 && shift <= 14;   // 2 x W bytes of u8 accumulators up to W = 16384, one 32 KB buffer above
   p.row_begin = row_begin; p.row_order = row_order; p.n_rows = n_rows; p.k = k;
   p.out_idx = out_idx; p.out_cnt = out_cnt; p.out_score = out_score;
@@ -996,19 +1057,8 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   p.ablate = 0;
   if (const char* ab = std::getenv("DPATHSIM_ABLATE")) p.ablate = std::atoi(ab);
   DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : sizeof(unsigned long long), st));
-  if (nw == 8) {   // 64 KB of u8 accumulators: 8-wave workgroups, two per CU
-    if (k <= 64) return launch<1, 8>(p, st);
-    if (k <= 128) return launch<2, 8>(p, st);
-    return launch<4, 8>(p, st);
-  }
-  if (nw == 1) {   // one wave per row
-    if (k <= 64) return launch<1, 1>(p, st);
-    if (k <= 128) return launch<2, 1>(p, st);
-    return launch<4, 1>(p, st);
-  }
-  if (k <= 64) return launch<1, 4>(p, st);
-  if (k <= 128) return launch<2, 4>(p, st);
-  return launch<4, 4>(p, st);
+  if (shift <= 13) return dispatch<true>(p, nw, k, st);   // 16-bit tile entries
+  return dispatch<false>(p, nw, k, st);
 }
 
 }  // extern "C"

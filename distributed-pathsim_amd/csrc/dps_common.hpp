@@ -92,6 +92,30 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
+template <class T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    T o = __shfl_xor(v, d, kWave);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// Flattened iteration over 64 lane-held segments: with `excl` the exclusive
+// prefix of the segment lengths (non-decreasing over lanes), the segment that
+// owns flattened entry i is the largest lane j with excl_j <= i (empty
+// segments are skipped because the next lane has the same prefix).
+__device__ __forceinline__ int wave_owner(uint32_t excl, uint32_t i) {
+  int j = 0;
+#pragma unroll
+  for (int step = kWave / 2; step > 0; step >>= 1) {
+    const uint32_t e = static_cast<uint32_t>(__shfl(static_cast<int>(excl), j + step, kWave));
+    if (e <= i) j += step;
+  }
+  return j;
+}
+
 // Ascending bitonic sort of one int per lane across the wave.
 __device__ __forceinline__ int wave_bitonic_sort(int v) {
   const int lane = lane_id();

@@ -447,25 +447,50 @@ __global__ __launch_bounds__(kBlock) void k_global_walks(const int64_t* __restri
                                                          int64_t* __restrict__ g,
                                                          int64_t* __restrict__ diag,
                                                          unsigned long long* __restrict__ stats) {
+  // A wave owns 64 consecutive rows, whose entries are one contiguous range of
+  // C: it walks that range in coalesced 64-entry strips (a lane finds its row
+  // by a 6-step search over the row offsets) and sums per row in LDS, so a
+  // heavy row costs strips, not one lane's serial loop.
+  __shared__ unsigned long long acc_g[kWavesPerBlock][kWave];
+  __shared__ unsigned long long acc_d[kWavesPerBlock][kWave];
   const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
   int64_t max_c = 0, max_d = 0, max_g = 0;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  const int64_t n_round = (n_rows + kWave - 1) / kWave * kWave;
-  for (int64_t x = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; x < n_round;
-       x += stride) {
-    if (x < n_rows) {
-      int64_t gx = 0, dx = 0;
-      for (int64_t j = c_ptr[x]; j < c_ptr[x + 1]; ++j) {
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  for (int64_t r0 = wave0 * kWave; r0 < n_rows; r0 += nwaves * kWave) {
+    const int64_t x = r0 + lane;
+    const int64_t base = c_ptr[r0];
+    const int64_t xe = x < n_rows ? x : n_rows;
+    const uint32_t excl = static_cast<uint32_t>(c_ptr[xe] - base);
+    const uint32_t total = static_cast<uint32_t>(
+        c_ptr[r0 + kWave < n_rows ? r0 + kWave : n_rows] - base);
+    acc_g[wave][lane] = 0;
+    acc_d[wave][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t e0 = 0; e0 < total; e0 += kWave) {
+      const uint32_t i = e0 + lane;
+      const int o = wave_owner(excl, i);   // every lane takes part in the shuffles
+      if (i < total) {
+        const int64_t j = base + i;
         const int64_t c = c_val[j];
-        gx += c * s[c_col[j]];
-        dx += c * c;
+        atomicAdd(&acc_g[wave][o], static_cast<unsigned long long>(c * s[c_col[j]]));
+        atomicAdd(&acc_d[wave][o], static_cast<unsigned long long>(c * c));
         max_c = c > max_c ? c : max_c;
       }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (x < n_rows) {
+      const int64_t gx = static_cast<int64_t>(acc_g[wave][lane]);
+      const int64_t dx = static_cast<int64_t>(acc_d[wave][lane]);
       g[x] = gx;
       if (diag) diag[x] = dx;
       max_d = dx > max_d ? dx : max_d;
       max_g = gx > max_g ? gx : max_g;
     }
+    __builtin_amdgcn_wave_barrier();
   }
   max_c = wave_max(max_c);
   max_d = wave_max(max_d);

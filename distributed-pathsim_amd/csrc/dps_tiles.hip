@@ -2,10 +2,13 @@
 // helpers of the reference-compatible class:
 //   dps_target_order   targets relabeled in ascending global walk g (stable
 //                      LSD radix sort) -- a pure layout choice;
-//   dps_ct_tiles_build C^T cut into target tiles of W = 2^shift labels, bucket
-//                      (v,t) = packed uint32 (C[y,v] << 16) | (label - t*W),
+//   dps_ct_tiles_build C^T cut into target tiles of W = 2^shift labels,
 //                      buckets [v][t], zero-padded to 16 bytes; per-bucket max
-//                      C and per-tile min g for the hot kernel's bounds;
+//                      C and per-tile min g for the hot kernel's bounds.
+//                      Entries: W <= 8192 -> packed uint16 (c << 13) | (label -
+//                      t*W) with C[y,v] split into pieces c <= 7 (the kernel's
+//                      adds are linear in C, so the pieces sum exactly); wider
+//                      tiles -> packed uint32 (C[y,v] << 16) | (label - t*W);
 //   dps_walk_row / dps_row_scores / dps_pair_count: one source row, as the
 //                      reference's run() loop computes it (:30-52).
 #include "dps_common.hpp"
@@ -34,6 +37,27 @@ __device__ __forceinline__ int64_t label_of(const int32_t* rank, int64_t y) {
 }
 
 constexpr int64_t kTileGminLds = 4096;   // tiles whose g minimum is reduced in LDS
+
+// Entry format (see the file header): 16-bit entries for shift <= 13.
+constexpr int kP16MaxShift = 13;
+constexpr uint32_t kP16MaxC = 7;
+__device__ __forceinline__ uint32_t n_pieces(bool p16, uint32_t c) {
+  return p16 ? (c + kP16MaxC - 1) / kP16MaxC : 1u;
+}
+// Write the entries of (c, local label) at entry index i (16- or 32-bit units).
+__device__ __forceinline__ void put_entry(bool p16, uint32_t* ent, int64_t i, uint32_t c,
+                                          uint32_t lab) {
+  if (!p16) {
+    ent[i] = (c << 16) | lab;
+    return;
+  }
+  uint16_t* e16 = reinterpret_cast<uint16_t*>(ent);
+  for (; c > 0; ++i) {
+    const uint32_t piece = c < kP16MaxC ? c : kP16MaxC;
+    e16[i] = static_cast<uint16_t>((piece << 13) | lab);
+    c -= piece;
+  }
+}
 
 __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict__ c_ptr,
                                                        const int32_t* __restrict__ c_col,
@@ -65,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
       const int32_t c = c_val[j];
       if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
       const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
-      atomicAdd(&cnt[b], 1u);
+      atomicAdd(&cnt[b], n_pieces(shift <= kP16MaxShift, static_cast<uint32_t>(c)));
       if (maxc) atomicMax(&maxc[b], static_cast<uint32_t>(c));
     }
   }
@@ -75,32 +99,38 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
       if (gmin_s[i] != ~0ull) atomicMin(&gmin[i], gmin_s[i]);
 }
 
-// Buckets are padded to a multiple of 4 entries (16 B) so the hot kernel's
-// 16-byte chunks never straddle two buckets; padding entries are 0 (C = 0).
-__global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, int64_t n) {
+// Buckets are padded to 16 B (4 uint32 or 8 uint16 entries) so the hot
+// kernel's 16-byte chunks never straddle two buckets; padding entries have C = 0.
+__global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, int64_t n,
+                                                   uint32_t per16) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * kBlock)
-    cnt[i] = (cnt[i] + 3u) & ~3u;
+    cnt[i] = (cnt[i] + per16 - 1u) & ~(per16 - 1u);
 }
 
 __global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__ off,
                                                      const uint32_t* __restrict__ cursor,
-                                                     int64_t n, uint32_t lab_mask,
+                                                     int64_t n, uint32_t lab_mask, bool p16,
                                                      uint32_t* __restrict__ ent) {
   // Padding entries have C = 0 (they add nothing) and a label that walks over
   // the tile's dwords, so the hot kernel's branch-free u8 adds of padding do not
   // pile onto one LDS bank.
   for (int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; b < n;
        b += static_cast<int64_t>(gridDim.x) * kBlock)
-    for (int64_t i = off[b] + cursor[b]; i < off[b + 1]; ++i)
-      ent[i] = (static_cast<uint32_t>(i) << 2) & lab_mask;
+    for (int64_t i = off[b] + cursor[b]; i < off[b + 1]; ++i) {
+      const uint32_t pad = (static_cast<uint32_t>(i) << 2) & lab_mask;
+      if (p16) reinterpret_cast<uint16_t*>(ent)[i] = static_cast<uint16_t>(pad);
+      else ent[i] = pad;
+    }
 }
 
+// tile_off in uint32 words (16-bit entries: entry offset / 2, always even).
 __global__ __launch_bounds__(kBlock) void k_tile_off32(const int64_t* __restrict__ p64,
-                                                       int64_t n, uint32_t* __restrict__ p32) {
+                                                       int64_t n, int wshift,
+                                                       uint32_t* __restrict__ p32) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i <= n;
        i += static_cast<int64_t>(gridDim.x) * kBlock)
-    p32[i] = static_cast<uint32_t>(p64[i]);
+    p32[i] = static_cast<uint32_t>(p64[i] >> wshift);
 }
 
 __global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restrict__ c_ptr,
@@ -120,9 +150,10 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restri
     const int64_t t = lab >> shift;
     for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
       const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
-      const uint32_t pos = atomicAdd(&cursor[b], 1u);
-      ent[off[b] + pos] =
-          (static_cast<uint32_t>(c_val[j]) << 16) | (static_cast<uint32_t>(lab) & ymask);
+      const uint32_t c = static_cast<uint32_t>(c_val[j]);
+      const bool p16 = shift <= kP16MaxShift;
+      const uint32_t pos = atomicAdd(&cursor[b], n_pieces(p16, c));
+      put_entry(p16, ent, off[b] + pos, c, static_cast<uint32_t>(lab) & ymask);
     }
   }
 }
@@ -148,6 +179,42 @@ __device__ __forceinline__ int64_t row_of_label(const int32_t* perm, int64_t lab
   return perm ? static_cast<int64_t>(perm[lab]) : lab;
 }
 
+// The labels of a block are walked 64 at a time per wave (lane = label), and
+// their C entries as one flattened list in 64-entry strips (wave_owner maps a
+// strip slot back to its label), so heavy rows do not serialise one wave.
+struct LabelStrip {
+  int64_t d;       // lane l: c_ptr[y_l] - excl_l (entry index = d_owner + i)
+  uint32_t excl;   // exclusive prefix of the row lengths
+  uint32_t total;  // entries of the 64 labels (wave-uniform)
+};
+
+__device__ __forceinline__ LabelStrip label_strip(const int64_t* __restrict__ c_ptr,
+                                                  const int32_t* __restrict__ perm, int64_t lab,
+                                                  int64_t l1, int64_t* y_out) {
+  int64_t beg = 0;
+  uint32_t len = 0;
+  int64_t y = -1;
+  if (lab < l1) {
+    y = row_of_label(perm, lab);
+    beg = c_ptr[y];
+    len = static_cast<uint32_t>(c_ptr[y + 1] - beg);
+  }
+  *y_out = y;
+  const uint32_t inc = wave_inclusive_sum(len);
+  LabelStrip S;
+  S.excl = inc - len;
+  S.total = readlane(inc, kWave - 1);
+  S.d = beg - static_cast<int64_t>(S.excl);
+  return S;
+}
+
+// Strip slot i of S: entry index j and owning lane o (all lanes must call).
+__device__ __forceinline__ int64_t strip_entry(const LabelStrip& S, uint32_t i, int* o) {
+  *o = wave_owner(S.excl, i);
+  const int64_t d = __shfl(S.d, *o, kWave);
+  return d + static_cast<int64_t>(i);
+}
+
 __global__ __launch_bounds__(kBlock) void k_tile_count_blk(
     const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
     const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm,
@@ -162,21 +229,28 @@ __global__ __launch_bounds__(kBlock) void k_tile_count_blk(
   __syncthreads();
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
+  const bool p16 = shift <= kP16MaxShift;
   const int64_t l0 = static_cast<int64_t>(blockIdx.x) * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
   const int64_t t = l0 >> shift;
   unsigned long long gm = ~0ull;
-  for (int64_t lab = l0 + wave; lab < l1; lab += kWavesPerBlock) {
-    const int64_t y = row_of_label(perm, lab);
-    if (g) gm = min(gm, static_cast<unsigned long long>(g[y]));
-    for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
-      const int32_t c = c_val[j];
-      if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
-      const int32_t v = c_col[j];
-      atomicAdd(&cnt_s[v], 1u);
-      atomicMax(&mx_s[v], static_cast<uint32_t>(c));
+  for (int64_t lb = l0 + wave * kWave; lb < l1; lb += kBlock) {
+    int64_t y;
+    const LabelStrip S = label_strip(c_ptr, perm, lb + lane, l1, &y);
+    if (g && y >= 0) gm = min(gm, static_cast<unsigned long long>(g[y]));
+    for (uint32_t e0 = 0; e0 < S.total; e0 += kWave) {
+      int o;
+      const int64_t j = strip_entry(S, e0 + lane, &o);
+      if (e0 + lane < S.total) {
+        const int32_t c = c_val[j];
+        if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
+        const int32_t v = c_col[j];
+        atomicAdd(&cnt_s[v], n_pieces(p16, static_cast<uint32_t>(c)));
+        atomicMax(&mx_s[v], static_cast<uint32_t>(c));
+      }
     }
   }
+  gm = wave_min(gm);
   if (lane == 0 && gm != ~0ull) atomicMin(&gmin_s, gm);
   __syncthreads();
   for (int64_t v = threadIdx.x; v < n_mids; v += kBlock) {
@@ -198,13 +272,20 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter_blk(
   __syncthreads();
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
+  const bool p16 = shift <= kP16MaxShift;
   const int64_t l0 = static_cast<int64_t>(blockIdx.x) * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
   const int64_t t = l0 >> shift;
   const uint32_t ymask = (1u << shift) - 1u;
-  for (int64_t lab = l0 + wave; lab < l1; lab += kWavesPerBlock) {
-    const int64_t y = row_of_label(perm, lab);
-    for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) atomicAdd(&cnt_s[c_col[j]], 1u);
+  for (int64_t lb = l0 + wave * kWave; lb < l1; lb += kBlock) {
+    int64_t y;
+    const LabelStrip S = label_strip(c_ptr, perm, lb + lane, l1, &y);
+    for (uint32_t e0 = 0; e0 < S.total; e0 += kWave) {
+      int o;
+      const int64_t j = strip_entry(S, e0 + lane, &o);
+      if (e0 + lane < S.total)
+        atomicAdd(&cnt_s[c_col[j]], n_pieces(p16, static_cast<uint32_t>(c_val[j])));
+    }
   }
   __syncthreads();
   for (int64_t v = threadIdx.x; v < n_mids; v += kBlock) {
@@ -213,13 +294,19 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter_blk(
     cnt_s[v] = 0;
   }
   __syncthreads();
-  for (int64_t lab = l0 + wave; lab < l1; lab += kWavesPerBlock) {
-    const int64_t y = row_of_label(perm, lab);
-    for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
-      const int32_t v = c_col[j];
-      const uint32_t pos = base_s[v] + atomicAdd(&cnt_s[v], 1u);
-      ent[off[v * T + t] + pos] =
-          (static_cast<uint32_t>(c_val[j]) << 16) | (static_cast<uint32_t>(lab) & ymask);
+  for (int64_t lb = l0 + wave * kWave; lb < l1; lb += kBlock) {
+    int64_t y;
+    const LabelStrip S = label_strip(c_ptr, perm, lb + lane, l1, &y);
+    for (uint32_t e0 = 0; e0 < S.total; e0 += kWave) {
+      int o;
+      const int64_t j = strip_entry(S, e0 + lane, &o);
+      if (e0 + lane < S.total) {
+        const int32_t v = c_col[j];
+        const uint32_t c = static_cast<uint32_t>(c_val[j]);
+        const uint32_t pos = base_s[v] + atomicAdd(&cnt_s[v], n_pieces(p16, c));
+        const uint32_t lab = static_cast<uint32_t>(lb + o) & ymask;
+        put_entry(p16, ent, off[v * T + t] + pos, c, lab);
+      }
     }
   }
 }
@@ -245,10 +332,16 @@ __global__ __launch_bounds__(kBlock) void k_walk_row(const int32_t* __restrict__
       const int64_t b = static_cast<int64_t>(src_col[j]) * T + t;
       const int cx = src_val[j];
       for (uint32_t i = off[b] + threadIdx.x; i < off[b + 1]; i += kBlock) {
-        const uint32_t e = ent[i];
-        const uint32_t lab = e & 0xFFFFu;
+        const uint32_t w = ent[i];
+        if (shift <= kP16MaxShift) {   // two 16-bit entries per word (W = P here)
+          const uint32_t lo = w & 0xFFFFu, hi = w >> 16;
+          if (lo >> 13) atomicAdd(&acc[lo & 0x1FFFu], cx * static_cast<int>(lo >> 13));
+          if (hi >> 13) atomicAdd(&acc[hi & 0x1FFFu], cx * static_cast<int>(hi >> 13));
+          continue;
+        }
+        const uint32_t lab = w & 0xFFFFu;
         if (static_cast<int>(lab) / P != part) continue;
-        atomicAdd(&acc[lab % P], cx * static_cast<int>(e >> 16));
+        atomicAdd(&acc[lab % P], cx * static_cast<int>(w >> 16));
       }
     }
     __syncthreads();
@@ -336,12 +429,16 @@ int dps_target_order(const int64_t* g, int64_t n_targets, int32_t key_bits, int3
   return DPS_OK;
 }
 
-int64_t dps_ct_tiles_ent_capacity(int64_t nnz, int64_t n_mids, int64_t n_targets,
-                                  int32_t tile_w) {
-  if (tile_w <= 0) return 0;
+int64_t dps_ct_tiles_ent_capacity(int64_t nnz, int64_t sum_c, int64_t n_mids,
+                                  int64_t n_targets, int32_t tile_w) {
+  if (tile_w <= 0 || nnz < 0 || sum_c < nnz) return 0;
   const int64_t T = (n_targets + tile_w - 1) / tile_w;
   const int64_t nb = n_mids * (T > 0 ? T : 1);
-  return nnz + 3 * (nb < nnz ? nb : nnz) + 4;
+  if (log2_exact(tile_w) > kP16MaxShift) return nnz + 3 * (nb < nnz ? nb : nnz) + 4;
+  // 16-bit entries: ceil(c/7) <= 1 + (c-1)/7 pieces per C entry, up to 7
+  // padding entries per non-empty bucket, two entries per uint32 word
+  const int64_t pieces = nnz + (sum_c - nnz + kP16MaxC - 1) / kP16MaxC;
+  return (pieces + 7 * (nb < pieces ? nb : pieces) + 1) / 2 + 4;
 }
 
 size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t tile_w) {
@@ -407,12 +504,13 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
         reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
     DPS_LAUNCHED();
   }
+  const bool p16 = shift <= kP16MaxShift;   // cnt, off64, cursor count entries
   if (nb > 0) {
-    k_round4<<<grid_for(nb, kBlock), kBlock, 0, st>>>(cnt, nb);
+    k_round4<<<grid_for(nb, kBlock), kBlock, 0, st>>>(cnt, nb, p16 ? 8u : 4u);
     DPS_LAUNCHED();
   }
   DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, off64, nb, sws, scan_ws, st));
-  k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, nb, tile_off);
+  k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, nb, p16 ? 1 : 0, tile_off);
   DPS_LAUNCHED();
   if (n_targets > 0 && nb > 0 && blk) {
     k_tile_scatter_blk<<<static_cast<unsigned>(nblk), kBlock, 0, st>>>(
@@ -426,7 +524,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   }
   if (nb > 0) {
     k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(
-        off64, cursor, nb, ((static_cast<uint32_t>(tile_w) - 1u) & ~3u), tile_ent);
+        off64, cursor, nb, ((static_cast<uint32_t>(tile_w) - 1u) & ~3u), p16, tile_ent);
     DPS_LAUNCHED();
   }
   return DPS_OK;

@@ -48,7 +48,7 @@ SIGNATURES = {
     "dps_target_order_workspace_size": (_sz, [_i64]),
     "dps_target_order": (C.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "dps_ct_tiles_workspace_size": (_sz, [_i64, _i64, _i32]),
-    "dps_ct_tiles_ent_capacity": (_i64, [_i64, _i64, _i64, _i32]),
+    "dps_ct_tiles_ent_capacity": (_i64, [_i64, _i64, _i64, _i64, _i32]),
     "dps_ct_tiles_build": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p,
                                      _p, _sz, _p]),
     "dps_cct_topk_workspace_size": (_sz, []),

@@ -159,7 +159,7 @@ class PathSimEngine:
             _lib.call("dps_global_walks", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NA, _ptr(s),
                       _ptr(g), _ptr(diag), _ptr(stats), st)
             mark("walks")
-            host = torch.cat([stats, ap_nnz, px_nnz]).cpu()      # sync 3: stats for key width
+            host = torch.cat([stats, ap_nnz, px_nnz, s.sum().view(1)]).cpu()   # sync 3: stats
             max_g = int(host[_lib.STAT_MAX_G])
             # A5 operand layout: targets relabeled by ascending g, then tiled C^T
             t_perm, t_rank = self._empty(NA, torch.int32), self._empty(NA, torch.int32)
@@ -173,7 +173,9 @@ class PathSimEngine:
             tile_off = self._empty(NV * T + 1, torch.int32)
             tile_maxc = self._empty(NV * T + 1, torch.int32)
             tile_gmin = self._empty(T, torch.int64)
-            ent_cap = _lib.size("dps_ct_tiles_ent_capacity", nnz_c, NV, NA, self.tile_w)
+            sum_s = int(host[_lib.STATS_LEN + 2])   # >= sum of C's values (s covers every AP row)
+            ent_cap = _lib.size("dps_ct_tiles_ent_capacity", nnz_c, max(sum_s, nnz_c), NV, NA,
+                                self.tile_w)
             if ent_cap >= 2 ** 32:
                 raise OverflowError("padded nnz(C) >= 2^32 exceeds the uint32 tile offsets")
             tile_ent = self._empty(ent_cap, torch.int32)

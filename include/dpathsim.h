@@ -163,25 +163,29 @@ int dps_target_order(const int64_t* g, int64_t n_targets, int32_t key_bits,
 /* ---------------------------------------------------------------------------
  * A5 operand layout, step 2: target-tiled transpose of C for the C.C^T kernels.
  * Target labels (t_rank[y], or y if t_rank == NULL) in [0, n_targets) are cut
- * into tiles of `tile_w` (power of two, 256..32768; the hot kernel keeps
- * acc int32[W] + bitmap + list uint16[W] of one tile in LDS per wave).
- * Bucket (v, t) holds the packed entries
- *   (C[y,v] << 16) | (label(y) - t*tile_w)   for every y of tile t with C[y,v] > 0,
- * stored contiguously in [v][t] order: bucket (v,t) is
- *   tile_ent[tile_off[v*T + t] .. tile_off[v*T + t + 1]),  T = ceil(n_targets/tile_w).
- * Every bucket is padded with zero entries to a multiple of 4 (16 bytes), so
- * bucket starts are 16-byte aligned and 16-byte chunks never straddle buckets.
- * tile_off uint32[n_mids*T + 1], tile_ent uint32[dps_ct_tiles_ent_capacity()].
+ * into tiles of `tile_w` (power of two, 256..65536; the hot kernel keeps one
+ * tile's packed u8 accumulators in LDS).  Bucket (v, t) holds, for every y of
+ * tile t with C[y,v] > 0, packed entries in one of two formats:
+ *   tile_w <= 8192: uint16 (c << 13) | (label(y) - t*tile_w), C[y,v] split into
+ *                   ceil(C/7) pieces c <= 7 that sum to C[y,v];
+ *   tile_w >= 16384: uint32 (C[y,v] << 16) | (label(y) - t*tile_w).
+ * Buckets are stored contiguously in [v][t] order: bucket (v,t) is the uint32
+ * words tile_ent[tile_off[v*T + t] .. tile_off[v*T + t + 1]),
+ * T = ceil(n_targets/tile_w).  Every bucket is padded with C = 0 entries to 16
+ * bytes, so bucket starts are 16-byte aligned and 16-byte chunks never straddle
+ * buckets.  tile_off uint32[n_mids*T + 1] (word offsets), tile_ent
+ * uint32[dps_ct_tiles_ent_capacity()].
  * Optional: tile_maxc uint32[n_mids*T + 1] = max C[y,v] per bucket;
  * tile_gmin int64[T] = min g[y] per tile (needs g).
  * Requires max C <= 65535 (else *status_dev = DPS_ERR_OVERFLOW).  Entry order
  * inside a bucket is unspecified (results are exact integer sums).
  * ------------------------------------------------------------------------- */
 size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t tile_w);
-/* Entries (uint32) tile_ent must hold for nnz = nnz(C[0:n_targets]): padding
- * included, plus one spare 16-byte chunk. */
-int64_t dps_ct_tiles_ent_capacity(int64_t nnz, int64_t n_mids, int64_t n_targets,
-                                  int32_t tile_w);
+/* uint32 words tile_ent must hold for nnz = nnz(C[0:n_targets]) and any
+ * sum_c >= the sum of those entries' values (e.g. sum(s)): padding included,
+ * plus one spare 16-byte chunk.  0 if sum_c < nnz. */
+int64_t dps_ct_tiles_ent_capacity(int64_t nnz, int64_t sum_c, int64_t n_mids,
+                                  int64_t n_targets, int32_t tile_w);
 int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
                        const int64_t* g, const int32_t* t_rank,
                        int64_t n_targets, int64_t n_mids, int32_t tile_w,

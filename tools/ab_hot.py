@@ -50,9 +50,10 @@ for W in Ws:
     c = eng.tensor("topk_ws")[:256].view(torch.int64).cpu().tolist()
     print(f"  counters per row: flushes {c[1]/R:.1f} candidates {c[2]/R:.1f} passers {c[3]/R:.1f} "
           f"tiles visited {c[4]/R:.1f} scanned {c[5]/R:.1f}", flush=True)
-    ws = c[5] * 4 / 4 if c[5] else 1   # wave-stages (4 waves per stage)
-    print(f"  per wave-stage: epilogue iterations {c[16]/(c[5]*4):.2f} prefilter passes {c[17]/(c[5]*4):.2f} "
-          f"exact passes {c[18]/(c[5]*4):.2f} extraction rounds {c[19]/(c[5]*4):.2f} "
-          f"fast loads {c[20]/(c[5]*4):.2f} slow loads {c[21]/(c[5]*4):.2f}", flush=True)
+    nw = 1 if W <= 8192 else (8 if W == 65536 else 4)   # waves per row (dps_cct_topk)
+    c[5] = c[5] or 1
+    print(f"  per wave-stage: epilogue iterations {c[16]/(c[5]*nw):.2f} prefilter passes {c[17]/(c[5]*nw):.2f} "
+          f"exact passes {c[18]/(c[5]*nw):.2f} extraction rounds {c[19]/(c[5]*nw):.2f} "
+          f"fast loads {c[20]/(c[5]*nw):.2f} slow loads {c[21]/(c[5]*nw):.2f}", flush=True)
     os.environ["DPATHSIM_ABLATE"] = "0"
 print(json.dumps(res))

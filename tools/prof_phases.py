@@ -24,7 +24,8 @@ for W in [int(w) for w in os.environ.get("AB_W", "16384,32768").split(",")]:
     ms16 = e0.elapsed_time(e1)
     c = eng.tensor("topk_ws")[:256].view(torch.int64).cpu().tolist()
     os.environ["DPATHSIM_ABLATE"] = "0"
-    stages = c[15] / 4
+    nw = 1 if W <= 8192 else (8 if W == 65536 else 4)   # waves per row (dps_cct_topk)
+    stages = c[15] / nw
     names = os.environ.get("PH_NAMES", "scatter,flush,barrier1,find,prefetch,epilogue,barrier2").split(",")
     tot = sum(c[8:8 + len(names)])
     print(f"W={W}: {ms:.1f} ms ({ms16:.1f} ms instrumented) for {R} rows; stages/row {stages / R:.1f}")
