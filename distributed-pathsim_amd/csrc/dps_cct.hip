@@ -51,7 +51,10 @@ constexpr bool kProfile = false;
 // Waves per workgroup NW is a template parameter: 4 (256 threads) for tiles
 // up to W = 32768, 8 (512 threads) for W = 65536, so that a CU always holds 16
 // waves (4 workgroups x 32 KB or 2 x 64 KB of accumulators).
-constexpr int kU = 4;               // 16-B chunk loads in flight per lane
+#ifndef DPS_KU
+#define DPS_KU 4
+#endif
+constexpr int kU = DPS_KU;          // 16-B chunk loads in flight per lane
 #ifndef DPS_EPIU
 #define DPS_EPIU 4
 #endif
@@ -242,7 +245,6 @@ struct Stage {
   int lnp;       // log2(number of passes): 0 u8, 1 u16, 2 u32
   int pass;
   int nb;        // batches of NW*64*kU chunks (0 under the no-scatter ablation)
-  int jc;        // venue cursor of issue(): venue of the last chunk block issued
   int64_t gq;    // lane s: smallest g of segment s of tile t
 };
 
@@ -253,42 +255,52 @@ struct Batch {
 
 // Issue the loads of batch b of stage S: chunk q -> lane (q mod 64*NW) of the
 // workgroup, kU chunks per lane.  Each load instruction reads 64 consecutive
-// chunks (q0 .. q0+63, q0 wave-uniform).  A wave-uniform venue cursor follows
-// the chunk blocks in order; when all 64 chunks of a load lie in the cursor's
-// venue (the common case: heavy venues own most chunks) the base address and
-// C[x,v] are scalars and the load costs a couple of VALU.  A load that straddles
-// venue boundaries resolves each lane's venue with chunk_venue().  Loads past
-// the stage's last chunk are skipped (uniform) and marked dead (c = 0).
+// chunks (q0 .. q0+63, q0 wave-uniform).  The venues owning its first and last
+// chunk come from two ballots over the venue lanes (pre_j <= q), so they are
+// scalars; when they agree (the common case: heavy venues own most chunks) the
+// base address and C[x,v] are scalars and the load costs a few VALU.  A load
+// straddling a few boundaries resolves each lane's venue with one readlane
+// compare per boundary; many boundaries take the shuffle search of
+// chunk_venue().  Loads past the stage's last chunk are skipped (uniform) and
+// marked dead (c = 0).
+constexpr int kFewBoundaries = 3;
+
 template <int NW>
 __device__ __forceinline__ void issue(Stage& S, int b, const uint32_t* __restrict__ ent,
                                       int wave, int lane, Batch& B, bool no_add,
                                       int p_ablate = 0, unsigned long long* p_counter = nullptr) {
+  const bool vl = lane < S.G.nv;
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const int q0 = b * (NW * kWave * kU) + u * (NW * kWave) + wave * kWave;   // wave-uniform
     B.c[u] = 0;
     B.e[u] = make_uint4(0, 0, 0, 0);
     if (q0 >= S.G.nq) continue;
-    int jn = S.jc + 1 < S.G.nv ? readlane(S.G.pre, S.jc + 1) : INT_MAX;
-    while (q0 >= jn) {
-      ++S.jc;
-      jn = S.jc + 1 < S.G.nv ? readlane(S.G.pre, S.jc + 1) : INT_MAX;
-    }
     const int q = q0 + lane;
     const bool live = q < S.G.nq;
-    uint32_t bj;
-    int cj;
-    if ((kProfile && (p_ablate & 8)) && lane == 0) atomicAdd(p_counter + (q0 + kWave - 1 < jn ? 20 : 21), 1ull);
-    if (q0 + kWave - 1 < jn) {
-      bj = readlane(S.G.base, S.jc);
-      cj = readlane(S.G.c, S.jc);
-    } else {
-      int sp[kSmallGroup];
+    const int qlast = min(q0 + kWave - 1, S.G.nq - 1);
+    const int jlo = __popcll(ballot(vl && S.G.pre <= q0)) - 1;
+    const int jhi = __popcll(ballot(vl && S.G.pre <= qlast)) - 1;
+    uint32_t bj = readlane(S.G.base, jlo);
+    int cj = readlane(S.G.c, jlo);
+    if ((kProfile && (p_ablate & 8)) && lane == 0) atomicAdd(p_counter + (jhi == jlo ? 20 : 21), 1ull);
+    if (jhi > jlo) {
+      if (jhi - jlo <= kFewBoundaries) {
+        for (int j = jlo + 1; j <= jhi; ++j) {   // wave-uniform loop
+          const bool ge = q >= readlane(S.G.pre, j);
+          const uint32_t bn = readlane(S.G.base, j);
+          const int cn = readlane(S.G.c, j);
+          bj = ge ? bn : bj;
+          cj = ge ? cn : cj;
+        }
+      } else {
+        int sp[kSmallGroup];
 #pragma unroll
-      for (int jj = 0; jj < kSmallGroup; ++jj) sp[jj] = readlane(S.G.pre, jj);
-      const int j = chunk_venue(S.G, sp, q);
-      bj = static_cast<uint32_t>(__shfl(static_cast<int>(S.G.base), j, kWave));
-      cj = __shfl(S.G.c, j, kWave);
+        for (int jj = 0; jj < kSmallGroup; ++jj) sp[jj] = readlane(S.G.pre, jj);
+        const int j = chunk_venue(S.G, sp, q);
+        bj = static_cast<uint32_t>(__shfl(static_cast<int>(S.G.base), j, kWave));
+        cj = __shfl(S.G.c, j, kWave);
+      }
     }
     B.e[u] = *reinterpret_cast<const uint4*>(ent + (live ? bj + 4u * static_cast<uint32_t>(q) : 0u));
     B.c[u] = live && !no_add ? cj : 0;
@@ -676,7 +688,6 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
     S.t = t;
     S.lnp = ub <= 0xFF ? 0 : ub <= 0xFFFF ? 1 : 2;
     S.pass = 0;
-    S.jc = 0;
     grp_set(S.G, lo, hi, w.c, d);
     if (no_scatter) S.G.nq = 0;
     S.nb = (S.G.nq + NW * kWave * kU - 1) / (NW * kWave * kU);
@@ -686,7 +697,6 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
   }
   S.G.base = 0; S.G.c = 0; S.G.pre = 0; S.G.nq = 0; S.G.nv = 1;   // no stage: dead loads only
   S.nb = 0;
-  S.jc = 0;
   return false;
 }
 
@@ -783,7 +793,11 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         // (one-wave rows too: skipping this LDS round trip measured 7 % slower)
         if (lane == 0) tau_s[n & 1][wave] = top.full() ? top.kth_s : -1.0;
         if (prof) ts[2] = __builtin_amdgcn_s_memtime();
+#ifdef DPS_NOBAR1
+        if constexpr (NW > 1) __syncthreads();   // one wave: its own LDS ops are in order
+#else
         __syncthreads();
+#endif
         if (prof) ts[3] = __builtin_amdgcn_s_memtime();
         double tm = tau_s[n & 1][0];
 #pragma unroll
@@ -794,7 +808,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         // stage's epilogue (pure LDS work unless the queue fills up)
         Stage nxt;
         bool have_n;
-        if (cur.pass + 1 < (1 << cur.lnp)) { nxt = cur; ++nxt.pass; nxt.jc = 0; have_n = true; }
+        if (cur.pass + 1 < (1 << cur.lnp)) { nxt = cur; ++nxt.pass; have_n = true; }
         else have_n = find_stage<NW>(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, nxt);
         if (!have_n) nxt.G.nq = 0;
         if (prof) ts[4] = __builtin_amdgcn_s_memtime();
@@ -802,6 +816,9 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         if (prof) ts[5] = __builtin_amdgcn_s_memtime();
         epilogue<KPL, NW>(p, acc, top, Q, cur, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh, mseg);
         if (prof) ts[6] = __builtin_amdgcn_s_memtime();
+#ifdef DPS_NOBAR2
+        if constexpr (NW > 1)
+#endif
         if (!p.dbuf) __syncthreads();   // one buffer: every wave has zeroed its quarter
         if (prof) {
           ts[7] = __builtin_amdgcn_s_memtime();
@@ -851,8 +868,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
               c = p.c_val[pb + j];
             }
             grp_set(S.G, lo, hi, c, d - g0 < kWave ? d - g0 : kWave);
-            S.jc = 0;
-            S.nb = (S.G.nq + NW * kWave * kU - 1) / (NW * kWave * kU);
+                    S.nb = (S.G.nq + NW * kWave * kU - 1) / (NW * kWave * kU);
             for (int b = 0; b < S.nb; ++b) {
               Batch B;
               issue<NW>(S, b, p.tile_ent, wave, lane, B, no_add);
