@@ -102,6 +102,13 @@ __device__ __forceinline__ T wave_min(T v) {
   return v;
 }
 
+// atomicMax on a hot device-wide address, skipped when a (possibly stale, but
+// monotone) read already shows a value >= v: a few record-breaking updates
+// instead of one serialised atomic per wave.
+__device__ __forceinline__ void atomic_max_filtered(unsigned long long* p, unsigned long long v) {
+  if (v > __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(p, v);
+}
+
 // Flattened iteration over 64 lane-held segments: with `excl` the exclusive
 // prefix of the segment lengths (non-decreasing over lanes), the segment that
 // owns flattened entry i is the largest lane j with excl_j <= i (empty

@@ -28,11 +28,16 @@ __global__ __launch_bounds__(kBlock) void k_extract(
   // A wave owns chunks of kExtractPer*64 consecutive edges: pass 1 classifies
   // them (flags kept as bitmasks), one atomicAdd per output list reserves the
   // chunk's slots, pass 2 writes the pairs in edge order within the chunk.
+  __shared__ unsigned long long cnt_s[2][kWavesPerBlock];
+  __shared__ unsigned long long base_s[2];
   const int lane = lane_id();
-  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int wave = threadIdx.x / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
   constexpr int64_t kChunk = static_cast<int64_t>(kExtractPer) * kWave;
-  for (int64_t c0 = wave0 * kChunk; c0 < n; c0 += nwaves * kChunk) {
+  // block-uniform trip count: every wave of a block reaches the barriers
+  const int64_t blk0 = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock * kChunk;
+  for (int64_t cb = blk0; cb < n; cb += nwaves * kChunk) {
+    const int64_t c0 = cb + wave * kChunk;
     uint32_t f_ap = 0, f_px = 0;
     int c_ap = 0, c_px = 0;
 #pragma unroll
@@ -52,13 +57,23 @@ __global__ __launch_bounds__(kBlock) void k_extract(
       c_ap += __popcll(m_ap);
       c_px += __popcll(m_px);
     }
-    unsigned long long b_ap = 0, b_px = 0;
-    if (lane == 0) {
-      if (c_ap) b_ap = atomicAdd(n_ap, static_cast<unsigned long long>(c_ap));
-      if (c_px) b_px = atomicAdd(n_px, static_cast<unsigned long long>(c_px));
+    // one reservation per block and list (the counters are hot addresses):
+    // wave w's slots follow waves 0..w-1 of the same block iteration
+    __syncthreads();   // the previous iteration's reads of cnt_s are done
+    if (lane == 0) { cnt_s[0][wave] = c_ap; cnt_s[1][wave] = c_px; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long t_ap = 0, t_px = 0;
+#pragma unroll
+      for (int w = 0; w < kWavesPerBlock; ++w) { t_ap += cnt_s[0][w]; t_px += cnt_s[1][w]; }
+      base_s[0] = t_ap ? atomicAdd(n_ap, t_ap) : 0ull;
+      base_s[1] = t_px ? atomicAdd(n_px, t_px) : 0ull;
     }
-    int64_t o_ap = static_cast<int64_t>(__shfl(b_ap, 0, kWave));
-    int64_t o_px = static_cast<int64_t>(__shfl(b_px, 0, kWave));
+    __syncthreads();
+    int64_t o_ap = static_cast<int64_t>(base_s[0]), o_px = static_cast<int64_t>(base_s[1]);
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w)
+      if (w < wave) { o_ap += cnt_s[0][w]; o_px += cnt_s[1][w]; }
 #pragma unroll
     for (int u = 0; u < kExtractPer; ++u) {
       const int64_t i = c0 + u * kWave + lane;
@@ -363,9 +378,17 @@ __global__ __launch_bounds__(kBlock) void k_expand_len(const int64_t* __restrict
       }
     }
   }
+  // one atomic per block on the (hot) total
+  __shared__ int64_t part[kWavesPerBlock];
   const int64_t wave_total = wave_sum(lane_total);
-  if (lane == 0 && e_total && wave_total)
-    atomicAdd(e_total, static_cast<unsigned long long>(wave_total));
+  if (lane == 0) part[threadIdx.x / kWave] = wave_total;
+  __syncthreads();
+  if (threadIdx.x == 0 && e_total) {
+    int64_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) t += part[w];
+    if (t) atomicAdd(e_total, static_cast<unsigned long long>(t));
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_expand(const int64_t* __restrict__ ap_ptr,
@@ -496,9 +519,9 @@ __global__ __launch_bounds__(kBlock) void k_global_walks(const int64_t* __restri
   max_d = wave_max(max_d);
   max_g = wave_max(max_g);
   if (lane == 0 && stats) {
-    atomicMax(&stats[DPS_STAT_MAX_C], static_cast<unsigned long long>(max_c));
-    atomicMax(&stats[DPS_STAT_MAX_DIAG], static_cast<unsigned long long>(max_d));
-    atomicMax(&stats[DPS_STAT_MAX_G], static_cast<unsigned long long>(max_g));
+    atomic_max_filtered(&stats[DPS_STAT_MAX_C], static_cast<unsigned long long>(max_c));
+    atomic_max_filtered(&stats[DPS_STAT_MAX_DIAG], static_cast<unsigned long long>(max_d));
+    atomic_max_filtered(&stats[DPS_STAT_MAX_G], static_cast<unsigned long long>(max_g));
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && stats)
     stats[DPS_STAT_NNZ_C] = static_cast<unsigned long long>(c_ptr[n_rows] - c_ptr[0]);
@@ -630,7 +653,7 @@ int dps_spgemm_expand_size(const int64_t* ap_ptr, const int32_t* ap_col, const i
   auto st = static_cast<hipStream_t>(stream);
   DPS_HIP_RET(hipMemsetAsync(e_total, 0, sizeof(int64_t), st));
   if (n_out_rows == 0) return DPS_OK;
-  k_expand_len<<<grid_for(n_out_rows, kBlock), kBlock, 0, st>>>(
+  k_expand_len<<<grid_for(n_out_rows, kBlock, 1024), kBlock, 0, st>>>(   // <= 1024 hot atomics
       ap_ptr, ap_col, rows, n_out_rows, px_ptr, nullptr,
       reinterpret_cast<unsigned long long*>(e_total));
   DPS_LAUNCHED();

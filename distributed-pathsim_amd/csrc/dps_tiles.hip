@@ -108,16 +108,17 @@ __global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, i
     cnt[i] = (cnt[i] + per16 - 1u) & ~(per16 - 1u);
 }
 
-__global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__ off,
+__global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__ off, int P,
                                                      const uint32_t* __restrict__ cursor,
                                                      int64_t n, uint32_t lab_mask, bool p16,
                                                      uint32_t* __restrict__ ent) {
-  // Padding entries have C = 0 (they add nothing) and a label that walks over
-  // the tile's dwords, so the hot kernel's branch-free u8 adds of padding do not
-  // pile onto one LDS bank.
+  // Bucket b spans off[b*P] .. off[(b+1)*P) (P parts per bucket), its first
+  // cursor[b] entries are real.  Padding entries have C = 0 (they add nothing)
+  // and a label that walks over the tile's dwords, so the hot kernel's
+  // branch-free u8 adds of padding do not pile onto one LDS bank.
   for (int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; b < n;
        b += static_cast<int64_t>(gridDim.x) * kBlock)
-    for (int64_t i = off[b] + cursor[b]; i < off[b + 1]; ++i) {
+    for (int64_t i = off[b * P] + cursor[b]; i < off[(b + 1) * P]; ++i) {
       const uint32_t pad = (static_cast<uint32_t>(i) << 2) & lab_mask;
       if (p16) reinterpret_cast<uint16_t*>(ent)[i] = static_cast<uint16_t>(pad);
       else ent[i] = pad;
@@ -125,12 +126,12 @@ __global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__
 }
 
 // tile_off in uint32 words (16-bit entries: entry offset / 2, always even).
-__global__ __launch_bounds__(kBlock) void k_tile_off32(const int64_t* __restrict__ p64,
+__global__ __launch_bounds__(kBlock) void k_tile_off32(const int64_t* __restrict__ p64, int P,
                                                        int64_t n, int wshift,
                                                        uint32_t* __restrict__ p32) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i <= n;
        i += static_cast<int64_t>(gridDim.x) * kBlock)
-    p32[i] = static_cast<uint32_t>(p64[i] >> wshift);
+    p32[i] = static_cast<uint32_t>(p64[i * P] >> wshift);
 }
 
 __global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restrict__ c_ptr,
@@ -167,6 +168,9 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restri
 // LDS cursors.  Entry order inside a bucket is unspecified either way.
 constexpr int kBlkMids = 8192;
 constexpr int kBlkLabels = 1024;
+// 16 waves per block (one 64-label group each): with 64 KB of LDS per block a
+// CU holds two blocks = 32 waves, enough to cover the latency of the gathers.
+constexpr int kBlkThreads = 1024;
 
 __global__ __launch_bounds__(kBlock) void k_tile_invert(const int32_t* __restrict__ rank,
                                                         int64_t n, int32_t* __restrict__ perm) {
@@ -215,16 +219,22 @@ __device__ __forceinline__ int64_t strip_entry(const LabelStrip& S, uint32_t i, 
   return d + static_cast<int64_t>(i);
 }
 
-__global__ __launch_bounds__(kBlock) void k_tile_count_blk(
+// Block (t, h) owns part h of tile t (labels_per_block labels, P parts per
+// tile).  Counting writes the block's per-venue piece counts and maxima to its
+// own slots cntp/mxp[(v*T + t)*P + h] -- no global atomics; k_tile_parts_fix
+// pads each bucket and reduces the maxima, and one exclusive scan over the
+// [v][t][h] order gives every part its base offset, so the scatter needs only
+// LDS cursors.
+__global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
     const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
     const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm,
     const int64_t* __restrict__ g, int64_t n_targets, int64_t n_mids, int shift, int64_t T,
-    int labels_per_block, uint32_t* __restrict__ cnt, uint32_t* __restrict__ maxc,
+    int labels_per_block, int P, uint32_t* __restrict__ cntp, uint32_t* __restrict__ mxp,
     unsigned long long* __restrict__ gmin, int32_t* __restrict__ status) {
   __shared__ uint32_t cnt_s[kBlkMids];
   __shared__ uint32_t mx_s[kBlkMids];
   __shared__ unsigned long long gmin_s;
-  for (int64_t v = threadIdx.x; v < n_mids; v += kBlock) { cnt_s[v] = 0; mx_s[v] = 0; }
+  for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) { cnt_s[v] = 0; mx_s[v] = 0; }
   if (threadIdx.x == 0) gmin_s = ~0ull;
   __syncthreads();
   const int lane = lane_id();
@@ -233,8 +243,9 @@ __global__ __launch_bounds__(kBlock) void k_tile_count_blk(
   const int64_t l0 = static_cast<int64_t>(blockIdx.x) * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
   const int64_t t = l0 >> shift;
+  const int64_t h = static_cast<int64_t>(blockIdx.x) % P;
   unsigned long long gm = ~0ull;
-  for (int64_t lb = l0 + wave * kWave; lb < l1; lb += kBlock) {
+  for (int64_t lb = l0 + wave * kWave; lb < l1; lb += kBlkThreads) {
     int64_t y;
     const LabelStrip S = label_strip(c_ptr, perm, lb + lane, l1, &y);
     if (g && y >= 0) gm = min(gm, static_cast<unsigned long long>(g[y]));
@@ -253,22 +264,41 @@ __global__ __launch_bounds__(kBlock) void k_tile_count_blk(
   gm = wave_min(gm);
   if (lane == 0 && gm != ~0ull) atomicMin(&gmin_s, gm);
   __syncthreads();
-  for (int64_t v = threadIdx.x; v < n_mids; v += kBlock) {
+  for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) {
     if (!cnt_s[v]) continue;
-    atomicAdd(&cnt[v * T + t], cnt_s[v]);
-    if (maxc) atomicMax(&maxc[v * T + t], mx_s[v]);
+    cntp[(v * T + t) * P + h] = cnt_s[v];
+    mxp[(v * T + t) * P + h] = mx_s[v];
   }
   if (threadIdx.x == 0 && gmin && gmin_s != ~0ull) atomicMin(&gmin[t], gmin_s);
 }
 
-__global__ __launch_bounds__(kBlock) void k_tile_scatter_blk(
+// Per bucket b: tot = real entries (kept in cnt[b] for the padding pass),
+// padding to 16 B added to the last part, maxc = max over the parts.
+__global__ __launch_bounds__(kBlock) void k_tile_parts_fix(uint32_t* __restrict__ cntp,
+                                                           const uint32_t* __restrict__ mxp,
+                                                           int64_t nb, int P, uint32_t per16,
+                                                           uint32_t* __restrict__ cnt,
+                                                           uint32_t* __restrict__ maxc) {
+  for (int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; b < nb;
+       b += static_cast<int64_t>(gridDim.x) * kBlock) {
+    uint32_t tot = 0, mx = 0;
+    for (int h = 0; h < P; ++h) {
+      tot += cntp[b * P + h];
+      mx = max(mx, mxp[b * P + h]);
+    }
+    cnt[b] = tot;
+    cntp[b * P + P - 1] += ((tot + per16 - 1u) & ~(per16 - 1u)) - tot;
+    if (maxc) maxc[b] = mx;
+  }
+}
+
+__global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
     const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
     const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm, int64_t n_targets,
-    int64_t n_mids, int shift, int64_t T, int labels_per_block,
-    const int64_t* __restrict__ off, uint32_t* __restrict__ cursor, uint32_t* __restrict__ ent) {
-  __shared__ uint32_t cnt_s[kBlkMids];
-  __shared__ uint32_t base_s[kBlkMids];
-  for (int64_t v = threadIdx.x; v < n_mids; v += kBlock) cnt_s[v] = 0;
+    int64_t n_mids, int shift, int64_t T, int labels_per_block, int P,
+    const int64_t* __restrict__ offp, uint32_t* __restrict__ ent) {
+  __shared__ uint32_t cur_s[kBlkMids];
+  for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) cur_s[v] = 0;
   __syncthreads();
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
@@ -276,25 +306,9 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter_blk(
   const int64_t l0 = static_cast<int64_t>(blockIdx.x) * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
   const int64_t t = l0 >> shift;
+  const int64_t h = static_cast<int64_t>(blockIdx.x) % P;
   const uint32_t ymask = (1u << shift) - 1u;
-  for (int64_t lb = l0 + wave * kWave; lb < l1; lb += kBlock) {
-    int64_t y;
-    const LabelStrip S = label_strip(c_ptr, perm, lb + lane, l1, &y);
-    for (uint32_t e0 = 0; e0 < S.total; e0 += kWave) {
-      int o;
-      const int64_t j = strip_entry(S, e0 + lane, &o);
-      if (e0 + lane < S.total)
-        atomicAdd(&cnt_s[c_col[j]], n_pieces(p16, static_cast<uint32_t>(c_val[j])));
-    }
-  }
-  __syncthreads();
-  for (int64_t v = threadIdx.x; v < n_mids; v += kBlock) {
-    const uint32_t n = cnt_s[v];
-    base_s[v] = n ? atomicAdd(&cursor[v * T + t], n) : 0u;
-    cnt_s[v] = 0;
-  }
-  __syncthreads();
-  for (int64_t lb = l0 + wave * kWave; lb < l1; lb += kBlock) {
+  for (int64_t lb = l0 + wave * kWave; lb < l1; lb += kBlkThreads) {
     int64_t y;
     const LabelStrip S = label_strip(c_ptr, perm, lb + lane, l1, &y);
     for (uint32_t e0 = 0; e0 < S.total; e0 += kWave) {
@@ -303,9 +317,9 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter_blk(
       if (e0 + lane < S.total) {
         const int32_t v = c_col[j];
         const uint32_t c = static_cast<uint32_t>(c_val[j]);
-        const uint32_t pos = base_s[v] + atomicAdd(&cnt_s[v], n_pieces(p16, c));
+        const uint32_t pos = atomicAdd(&cur_s[v], n_pieces(p16, c));
         const uint32_t lab = static_cast<uint32_t>(lb + o) & ymask;
-        put_entry(p16, ent, off[v * T + t] + pos, c, lab);
+        put_entry(p16, ent, offp[(v * T + t) * P + h] + pos, c, lab);
       }
     }
   }
@@ -399,6 +413,12 @@ int log2_exact(int32_t w) {
   return (1 << s) == w ? s : -1;
 }
 
+// Parts per tile of the block-local build (1 on the global-atomic path).
+int64_t tile_parts(int64_t n_mids, int32_t tile_w) {
+  if (n_mids > kBlkMids) return 1;
+  return tile_w > kBlkLabels ? tile_w / kBlkLabels : 1;
+}
+
 }  // namespace
 }  // namespace dps
 
@@ -445,11 +465,14 @@ size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t ti
   if (tile_w <= 0) return 0;
   const int64_t T = (n_targets + tile_w - 1) / tile_w;
   const int64_t nb = n_mids * (T > 0 ? T : 1);
+  const int64_t np = nb * tile_parts(n_mids, tile_w);   // part slots (blk path) or buckets
   size_t s = 0;
   s += align_up(static_cast<size_t>(nb + 1) * sizeof(uint32_t));  // cnt
   s += align_up(static_cast<size_t>(nb + 1) * sizeof(uint32_t));  // cursor
-  s += align_up(static_cast<size_t>(nb + 1) * sizeof(int64_t));   // off64
-  s += align_up(scan_workspace_size(nb + 1));
+  s += align_up(static_cast<size_t>(np + 1) * sizeof(int64_t));   // off64 (per part)
+  s += align_up(scan_workspace_size(np + 1));
+  s += align_up(static_cast<size_t>(np + 1) * sizeof(uint32_t));  // cntp
+  s += align_up(static_cast<size_t>(np + 1) * sizeof(uint32_t));  // mxp
   s += align_up(static_cast<size_t>(n_targets > 0 ? n_targets : 1) * sizeof(int32_t));  // perm
   return s + 1024;
 }
@@ -472,59 +495,85 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   auto st = static_cast<hipStream_t>(stream);
   const int64_t T = (n_targets + tile_w - 1) / tile_w;
   const int64_t nb = n_mids * T;
+  const bool blk = n_mids <= kBlkMids;   // block-local LDS counting, parts per tile
+  const int P = static_cast<int>(tile_parts(n_mids, tile_w));
+  const int64_t np = nb * P;
   Carve c(ws, ws_bytes);
   uint32_t* cnt = c.take<uint32_t>(nb + 1);
   uint32_t* cursor = c.take<uint32_t>(nb + 1);
-  int64_t* off64 = c.take<int64_t>(nb + 1);
-  const size_t scan_ws = scan_workspace_size(nb + 1);
+  int64_t* off64 = c.take<int64_t>(np + 1);
+  const size_t scan_ws = scan_workspace_size(np + 1);
   void* sws = c.take<char>(scan_ws);
+  uint32_t* cntp = c.take<uint32_t>(np + 1);
+  uint32_t* mxp = c.take<uint32_t>(np + 1);
   int32_t* perm = c.take<int32_t>(n_targets > 0 ? n_targets : 1);
   DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "tiles workspace carve failed");
-  const bool blk = n_mids <= kBlkMids;   // block-local LDS counting
   const int lpb = tile_w < kBlkLabels ? tile_w : kBlkLabels;
   const int64_t nblk = (n_targets + lpb - 1) / lpb;
+  const bool p16 = shift <= kP16MaxShift;   // counts and offsets are in entries
+  const uint32_t per16 = p16 ? 8u : 4u;
   if (blk && t_rank && n_targets > 0) {
     k_tile_invert<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(t_rank, n_targets, perm);
     DPS_LAUNCHED();
   }
   const int32_t* perm_or_null = t_rank ? perm : nullptr;
   if (status_dev) DPS_HIP_RET(hipMemsetAsync(status_dev, 0, sizeof(int32_t), st));
+  if (tile_gmin && T > 0) DPS_HIP_RET(hipMemsetAsync(tile_gmin, 0x7F, T * sizeof(int64_t), st));
+  if (blk) {
+    DPS_HIP_RET(hipMemsetAsync(cntp, 0, (np + 1) * sizeof(uint32_t), st));
+    DPS_HIP_RET(hipMemsetAsync(mxp, 0, (np + 1) * sizeof(uint32_t), st));
+    if (tile_maxc) DPS_HIP_RET(hipMemsetAsync(tile_maxc + nb, 0, sizeof(uint32_t), st));
+    if (n_targets > 0 && nb > 0) {
+      k_tile_count_blk<<<static_cast<unsigned>(nblk), kBlkThreads, 0, st>>>(
+          c_ptr, c_col, c_val, perm_or_null, tile_gmin ? g : nullptr, n_targets, n_mids, shift, T,
+          lpb, P, cntp, mxp, reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
+      DPS_LAUNCHED();
+    }
+    if (nb > 0) {
+      k_tile_parts_fix<<<grid_for(nb, kBlock), kBlock, 0, st>>>(cntp, mxp, nb, P, per16, cnt,
+                                                                 tile_maxc);
+      DPS_LAUNCHED();
+    }
+    DPS_HIP_RET(scan_exclusive<uint32_t>(cntp, off64, np, sws, scan_ws, st));
+    k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, P, nb, p16 ? 1 : 0, tile_off);
+    DPS_LAUNCHED();
+    if (n_targets > 0 && nb > 0) {
+      k_tile_scatter_blk<<<static_cast<unsigned>(nblk), kBlkThreads, 0, st>>>(
+          c_ptr, c_col, c_val, perm_or_null, n_targets, n_mids, shift, T, lpb, P, off64, tile_ent);
+      DPS_LAUNCHED();
+    }
+    if (nb > 0) {
+      k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(
+          off64, P, cnt, nb, ((static_cast<uint32_t>(tile_w) - 1u) & ~3u), p16, tile_ent);
+      DPS_LAUNCHED();
+    }
+    return DPS_OK;
+  }
+  // many mids: global-atomic counting sort into (v, t) buckets
   DPS_HIP_RET(hipMemsetAsync(cnt, 0, (nb + 1) * sizeof(uint32_t), st));
   DPS_HIP_RET(hipMemsetAsync(cursor, 0, (nb + 1) * sizeof(uint32_t), st));
   if (tile_maxc) DPS_HIP_RET(hipMemsetAsync(tile_maxc, 0, (nb + 1) * sizeof(uint32_t), st));
-  if (tile_gmin && T > 0) DPS_HIP_RET(hipMemsetAsync(tile_gmin, 0x7F, T * sizeof(int64_t), st));
-  if (n_targets > 0 && nb > 0 && blk) {
-    k_tile_count_blk<<<static_cast<unsigned>(nblk), kBlock, 0, st>>>(
-        c_ptr, c_col, c_val, perm_or_null, tile_gmin ? g : nullptr, n_targets, n_mids, shift, T,
-        lpb, cnt, tile_maxc, reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
-    DPS_LAUNCHED();
-  } else if (n_targets > 0 && nb > 0) {
+  if (n_targets > 0 && nb > 0) {
     k_tile_count<<<grid_for(n_targets * kWave, kBlock, 2048), kBlock, 0, st>>>(
         c_ptr, c_col, c_val, t_rank, g, n_targets, shift, T, cnt, tile_maxc,
         reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
     DPS_LAUNCHED();
   }
-  const bool p16 = shift <= kP16MaxShift;   // cnt, off64, cursor count entries
   if (nb > 0) {
-    k_round4<<<grid_for(nb, kBlock), kBlock, 0, st>>>(cnt, nb, p16 ? 8u : 4u);
+    k_round4<<<grid_for(nb, kBlock), kBlock, 0, st>>>(cnt, nb, per16);
     DPS_LAUNCHED();
   }
   DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, off64, nb, sws, scan_ws, st));
-  k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, nb, p16 ? 1 : 0, tile_off);
+  k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, 1, nb, p16 ? 1 : 0, tile_off);
   DPS_LAUNCHED();
-  if (n_targets > 0 && nb > 0 && blk) {
-    k_tile_scatter_blk<<<static_cast<unsigned>(nblk), kBlock, 0, st>>>(
-        c_ptr, c_col, c_val, perm_or_null, n_targets, n_mids, shift, T, lpb, off64, cursor,
-        tile_ent);
-    DPS_LAUNCHED();
-  } else if (n_targets > 0 && nb > 0) {
+  if (n_targets > 0 && nb > 0) {
     k_tile_scatter<<<grid_for(n_targets * kWave, kBlock), kBlock, 0, st>>>(
         c_ptr, c_col, c_val, t_rank, n_targets, shift, T, off64, cursor, tile_ent);
     DPS_LAUNCHED();
   }
   if (nb > 0) {
     k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(
-        off64, cursor, nb, ((static_cast<uint32_t>(tile_w) - 1u) & ~3u), p16, tile_ent);
+        off64, 1, cursor, nb, ((static_cast<uint32_t>(tile_w) - 1u) & ~3u), p16, tile_ent);
     DPS_LAUNCHED();
   }
   return DPS_OK;
