@@ -6,32 +6,31 @@
 //   C      CSR over author rows: int64 row_ptr, int32 col (venue), int32 val.
 //   tiles  C^T cut into target tiles of W = 2^shift labels (targets relabeled
 //          in ascending global walk g, dps_target_order).  Bucket (v,t) holds
-//          packed uint32 entries (C[y,v] << 16) | (label(y) - t*W), buckets
-//          stored [v][t], each padded with zero entries to 16 bytes.
+//          packed entries -- W <= 8192: uint16 (c << 13) | (label - t*W), counts
+//          split into pieces c <= 7 (P16); wider: uint32 (C << 16) | (label -
+//          t*W) -- stored [v][t], each bucket padded to 16 bytes.
 //   g_t    g in label order (ascending), tile_maxc max C per bucket.
 //
-// One 256-thread workgroup (4 waves) owns one source row x at a time
-// (persistent grid, rows dequeued from an atomic counter).  For every target
+// Default shape (W = 8192): one wave owns one source row at a time (persistent
+// grid of single-wave workgroups, rows dequeued from an atomic counter,
+// heaviest first); W >= 16384: 4 or 8 waves share a row.  For every target
 // tile t in ascending g:
-//   bound     UB = sum_v C[x,v] * maxc[v,t].  The workgroup shares tau, the
-//             best k-th score any of its waves holds; mneed = the smallest M
-//             whose score against the tile's smallest g reaches tau.  UB <
-//             mneed: no target of the tile can enter the top-k, skip it.
-//   scatter   the row's buckets (v,t) are flattened into 16-byte chunks spread
-//             over all 256 lanes; acc[y] += C[x,v]*C[y,v] with no-return
-//             ds_add_u32 into PACKED u16 accumulators (two targets per dword).
-//             UB <= 65535 proves no u16 lane can carry into its neighbour;
-//             tiles with a larger bound run "wide": two sub-passes over half
-//             the targets each, one int32 per target.
-//   epilogue  each wave scans a quarter of the accumulator (ds_read_b128),
-//             zeroes it in the same pass and keeps targets whose M reaches the
-//             threshold of their 1/64-tile segment (mseg: the same bound, with
-//             the segment's smallest g -- targets are g-sorted, so this is
-//             nearly exact and needs no global load).  Survivors are scored
-//             exactly: double(2M) / double(gx + gy), one IEEE division, into
-//             the wave's register top-k (lane i holds rank i).
-// At the row end wave 0 merges the four wave lists, then writes the ranked
-// entries, the zero-score fill (reference target order) and empty slots.
+//   bound     UB = sum_v C[x,v] * maxc[v,t].  tau = the best k-th score held;
+//             mneed = the smallest M whose score against the tile's smallest g
+//             reaches tau.  UB < mneed: no target of the tile can enter the
+//             top-k, skip it.
+//   scatter   the row's buckets (v,t) are flattened into 16-byte chunks, 64
+//             per load instruction; acc[y] += C[x,v]*c with no-return
+//             ds_add_u32 into PACKED u8 accumulators (four targets per dword)
+//             when UB <= 255, else u16 / u32 passes over parts of the tile.
+//   epilogue  the accumulator is scanned (ds_read_b128) and zeroed in the same
+//             pass; targets whose M reaches the threshold of their 1024-target
+//             segment are queued and scored exactly: double(2M) / double(gx +
+//             gy), one IEEE division, into the register top-k (lane i holds
+//             rank i).
+// At the row end the waves' lists are merged (one-wave rows write straight
+// from registers), then the ranked entries, the zero-score fill (reference
+// target order) and empty slots are written.
 #include "dps_common.hpp"
 
 #include <cstdlib>
