@@ -714,7 +714,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
   const uint32_t lab_mask = ((1u << p.shift) - 1u) & ~3u;
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
-  const int wave = tid / kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);   // wave-uniform (SGPR)
   const int nbuf = 1 << (p.shift - 2);        // accumulator dwords per stage buffer
   // threshold segments of min(1024, W/4) targets: one epilogue iteration each
   const int seg_shift = p.shift - 2 < 10 ? p.shift - 2 : 10;
