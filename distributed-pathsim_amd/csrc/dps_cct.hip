@@ -6,9 +6,10 @@
 //   C      CSR over author rows: int64 row_ptr, int32 col (venue), int32 val.
 //   tiles  C^T cut into target tiles of W = 2^shift labels (targets relabeled
 //          in ascending global walk g, dps_target_order).  Bucket (v,t) holds
-//          packed entries -- W <= 8192: uint16 (c << 13) | (label - t*W), counts
-//          split into pieces c <= 7 (P16); wider: uint32 (C << 16) | (label -
-//          t*W) -- stored [v][t], each bucket padded to 16 bytes.
+//          packed entries -- W <= 8192: uint16 (l << 3) | e, l = label - t*W,
+//          one power-of-two piece 2^e of C[y,v] (P16; e = 6, 7 at l % 4 == 3
+//          are padding codes); wider: uint32 (C << 16) | (label - t*W) --
+//          stored [v][t], each bucket padded to 16 bytes.
 //   g_t    g in label order (ascending), tile_maxc max C per bucket.
 //
 // Default shape (W = 8192): one wave owns one source row at a time (persistent
@@ -330,14 +331,21 @@ __device__ __forceinline__ void acc_add(uint32_t* acc, uint32_t yl, uint32_t ce,
   __hip_atomic_fetch_add(dst, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// A word of entries: two 16-bit entries (c << 13 | label) when P16, else one
-// 32-bit entry (C << 16 | label).
+// A word of entries: two 16-bit entries (label << 3 | e) when P16 (padding
+// codes e >= 6 at label % 4 == 3 add nothing here), else one 32-bit entry
+// (C << 16 | label).
+__device__ __forceinline__ void acc_add_p16(uint32_t* acc, uint32_t h, int c, int lnp, int pass,
+                                            int shift) {
+  const uint32_t e = h & 7u, yl = (h >> 3) & 0x1FFFu;
+  if ((yl & 3u) == 3u && e >= 6u) return;
+  acc_add(acc, yl, 1u << e, c, lnp, pass, shift);
+}
 template <bool P16>
 __device__ __forceinline__ void acc_add_word(uint32_t* acc, uint32_t w, int c, int lnp, int pass,
                                              int shift) {
   if constexpr (P16) {
-    acc_add(acc, w & 0x1FFFu, (w >> 13) & 7u, c, lnp, pass, shift);
-    acc_add(acc, (w >> 16) & 0x1FFFu, w >> 29, c, lnp, pass, shift);
+    acc_add_p16(acc, w & 0xFFFFu, c, lnp, pass, shift);
+    acc_add_p16(acc, w >> 16, c, lnp, pass, shift);
   } else {
     acc_add(acc, w & 0xFFFFu, w >> 16, c, lnp, pass, shift);
   }
@@ -369,16 +377,20 @@ __device__ __forceinline__ void add_u8(uint32_t buf, uint32_t e, uint32_t c, uin
                          add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// The same for a word of two 16-bit entries (c << 13) | label (W <= 8192): the
-// low entry's byte shift is (w << 3) mod 32, the high one's (w >> 13) & 24.
+// The same for a word of two 16-bit entries (label << 3) | e (W <= 8192): the
+// entry's low five bits are 8*(label % 4) + e, exactly the shift that puts
+// C * 2^e into the target's byte, and v_lshlrev reads only those five bits --
+// no multiply, no mask: seven VALU per word.  Padding groups add C * 2^32 to
+// one dword, i.e. nothing (dps_tiles.hip).
 __device__ __forceinline__ void add_u8_p16(uint32_t buf, uint32_t w, uint32_t c,
                                            uint32_t lab_mask) {
-  const uint32_t alo = __umul24(c, (w >> 13) & 7u) << ((w << 3) & 24u);
-  const uint32_t ahi = __umul24(c, w >> 29) << ((w >> 13) & 24u);
-  __hip_atomic_fetch_add(reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(buf | (w & lab_mask))),
-                         alo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const uint32_t alo = c << (w & 31u);
+  const uint32_t ahi = c << ((w >> 16) & 31u);
   __hip_atomic_fetch_add(
-      reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(buf | ((w >> 16) & lab_mask))), ahi,
+      reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(buf | ((w >> 3) & lab_mask))), alo,
+      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_add(
+      reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(buf | ((w >> 19) & lab_mask))), ahi,
       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 

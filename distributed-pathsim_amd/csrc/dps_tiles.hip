@@ -5,10 +5,13 @@
 //   dps_ct_tiles_build C^T cut into target tiles of W = 2^shift labels,
 //                      buckets [v][t], zero-padded to 16 bytes; per-bucket max
 //                      C and per-tile min g for the hot kernel's bounds.
-//                      Entries: W <= 8192 -> packed uint16 (c << 13) | (label -
-//                      t*W) with C[y,v] split into pieces c <= 7 (the kernel's
-//                      adds are linear in C, so the pieces sum exactly); wider
-//                      tiles -> packed uint32 (C[y,v] << 16) | (label - t*W);
+//                      Entries: W <= 8192 -> packed uint16 (l << 3) | e, l =
+//                      label - t*W, one piece of value 2^e: C[y,v] is split
+//                      into power-of-two pieces (e <= 7; e <= 5 when l % 4 == 3,
+//                      since e = 6, 7 with l % 4 == 3 are the padding codes) --
+//                      the kernel's adds are linear in C, so the pieces sum
+//                      exactly; wider tiles -> packed uint32 (C[y,v] << 16) |
+//                      (label - t*W);
 //   dps_walk_row / dps_row_scores / dps_pair_count: one source row, as the
 //                      reference's run() loop computes it (:30-52).
 #include "dps_common.hpp"
@@ -39,10 +42,26 @@ __device__ __forceinline__ int64_t label_of(const int32_t* rank, int64_t y) {
 constexpr int64_t kTileGminLds = 4096;   // tiles whose g minimum is reduced in LDS
 
 // Entry format (see the file header): 16-bit entries for shift <= 13.
+// A 16-bit entry (l << 3) | e adds C[x,v] * 2^e to target l: in the hot
+// kernel's packed-u8 accumulators that is C[x,v] << (8*(l % 4) + e) -- the
+// entry's low five bits ARE the shift.  Codes e = 6, 7 at l % 4 == 3 are
+// reserved for padding (real pieces there stop at 2^5): a bucket's padding is
+// groups of {2^7, 2^7} or {2^7, 2^6, 2^6} on one dword, each adding
+// C[x,v] * 2^32 == 0 to it, so padding needs no multiply by a zero count.
 constexpr int kP16MaxShift = 13;
-constexpr uint32_t kP16MaxC = 7;
-__device__ __forceinline__ uint32_t n_pieces(bool p16, uint32_t c) {
-  return p16 ? (c + kP16MaxC - 1) / kP16MaxC : 1u;
+__device__ __forceinline__ uint32_t p16_max_e(uint32_t lab) { return (lab & 3u) == 3u ? 5u : 7u; }
+__device__ __forceinline__ uint32_t n_pieces(bool p16, uint32_t c, uint32_t lab) {
+  if (!p16) return 1u;
+  const uint32_t me = p16_max_e(lab);
+  return (c >> me) + static_cast<uint32_t>(__popc(c & ((1u << me) - 1u)));
+}
+// Bucket size in entries after padding to 16 B (4 uint32 / 8 uint16 entries).
+// 16-bit padding comes in groups of two or three entries, so a single padding
+// entry is never needed: such a bucket takes nine.
+__device__ __forceinline__ uint32_t padded_count(uint32_t tot, uint32_t per16) {
+  uint32_t r = (tot + per16 - 1u) & ~(per16 - 1u);
+  if (per16 == 8u && r - tot == 1u) r += 8u;
+  return r;
 }
 // Write the entries of (c, local label) at entry index i (16- or 32-bit units).
 __device__ __forceinline__ void put_entry(bool p16, uint32_t* ent, int64_t i, uint32_t c,
@@ -52,11 +71,10 @@ __device__ __forceinline__ void put_entry(bool p16, uint32_t* ent, int64_t i, ui
     return;
   }
   uint16_t* e16 = reinterpret_cast<uint16_t*>(ent);
-  for (; c > 0; ++i) {
-    const uint32_t piece = c < kP16MaxC ? c : kP16MaxC;
-    e16[i] = static_cast<uint16_t>((piece << 13) | lab);
-    c -= piece;
-  }
+  const uint32_t me = p16_max_e(lab);
+  for (uint32_t n = c >> me; n > 0; --n) e16[i++] = static_cast<uint16_t>((lab << 3) | me);
+  for (uint32_t r = c & ((1u << me) - 1u); r != 0; r &= r - 1u)
+    e16[i++] = static_cast<uint16_t>((lab << 3) | static_cast<uint32_t>(__ffs(r) - 1));
 }
 
 __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict__ c_ptr,
@@ -89,7 +107,8 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
       const int32_t c = c_val[j];
       if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
       const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
-      atomicAdd(&cnt[b], n_pieces(shift <= kP16MaxShift, static_cast<uint32_t>(c)));
+      atomicAdd(&cnt[b], n_pieces(shift <= kP16MaxShift, static_cast<uint32_t>(c),
+                                  static_cast<uint32_t>(label_of(rank, y))));
       if (maxc) atomicMax(&maxc[b], static_cast<uint32_t>(c));
     }
   }
@@ -105,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, i
                                                    uint32_t per16) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * kBlock)
-    cnt[i] = (cnt[i] + per16 - 1u) & ~(per16 - 1u);
+    cnt[i] = padded_count(cnt[i], per16);
 }
 
 __global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__ off, int P,
@@ -117,12 +136,23 @@ __global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__
   // and a label that walks over the tile's dwords, so the hot kernel's
   // branch-free u8 adds of padding do not pile onto one LDS bank.
   for (int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; b < n;
-       b += static_cast<int64_t>(gridDim.x) * kBlock)
-    for (int64_t i = off[b * P] + cursor[b]; i < off[(b + 1) * P]; ++i) {
-      const uint32_t pad = (static_cast<uint32_t>(i) << 2) & lab_mask;
-      if (p16) reinterpret_cast<uint16_t*>(ent)[i] = static_cast<uint16_t>(pad);
-      else ent[i] = pad;
+       b += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int64_t i0 = off[b * P] + cursor[b];
+    const int64_t np = off[(b + 1) * P] - i0;
+    for (int64_t k = 0; k < np; ++k) {
+      const int64_t i = i0 + k;
+      if (!p16) {
+        ent[i] = (static_cast<uint32_t>(i) << 2) & lab_mask;
+        continue;
+      }
+      // groups on one dword: {7, 6, 6} first when the count is odd, then {7, 7}
+      const bool odd = (np & 1) != 0;
+      const int64_t grp = odd ? (k < 3 ? 0 : 1 + (k - 3) / 2) : k / 2;
+      const uint32_t e = (odd && (k == 1 || k == 2)) ? 6u : 7u;
+      const uint32_t lab = ((static_cast<uint32_t>(i0 + 2 * grp) << 2) & lab_mask) | 3u;
+      reinterpret_cast<uint16_t*>(ent)[i] = static_cast<uint16_t>((lab << 3) | e);
     }
+  }
 }
 
 // tile_off in uint32 words (16-bit entries: entry offset / 2, always even).
@@ -153,8 +183,9 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restri
       const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
       const uint32_t c = static_cast<uint32_t>(c_val[j]);
       const bool p16 = shift <= kP16MaxShift;
-      const uint32_t pos = atomicAdd(&cursor[b], n_pieces(p16, c));
-      put_entry(p16, ent, off[b] + pos, c, static_cast<uint32_t>(lab) & ymask);
+      const uint32_t l = static_cast<uint32_t>(lab) & ymask;
+      const uint32_t pos = atomicAdd(&cursor[b], n_pieces(p16, c, l));
+      put_entry(p16, ent, off[b] + pos, c, l);
     }
   }
 }
@@ -256,7 +287,8 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
         const int32_t c = c_val[j];
         if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
         const int32_t v = c_col[j];
-        atomicAdd(&cnt_s[v], n_pieces(p16, static_cast<uint32_t>(c)));
+        atomicAdd(&cnt_s[v], n_pieces(p16, static_cast<uint32_t>(c),
+                                      static_cast<uint32_t>(lb + o)));
         atomicMax(&mx_s[v], static_cast<uint32_t>(c));
       }
     }
@@ -287,7 +319,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_parts_fix(uint32_t* __restrict_
       mx = max(mx, mxp[b * P + h]);
     }
     cnt[b] = tot;
-    cntp[b * P + P - 1] += ((tot + per16 - 1u) & ~(per16 - 1u)) - tot;
+    cntp[b * P + P - 1] += padded_count(tot, per16) - tot;
     if (maxc) maxc[b] = mx;
   }
 }
@@ -317,8 +349,8 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
       if (e0 + lane < S.total) {
         const int32_t v = c_col[j];
         const uint32_t c = static_cast<uint32_t>(c_val[j]);
-        const uint32_t pos = atomicAdd(&cur_s[v], n_pieces(p16, c));
         const uint32_t lab = static_cast<uint32_t>(lb + o) & ymask;
+        const uint32_t pos = atomicAdd(&cur_s[v], n_pieces(p16, c, lab));
         put_entry(p16, ent, offp[(v * T + t) * P + h] + pos, c, lab);
       }
     }
@@ -348,9 +380,13 @@ __global__ __launch_bounds__(kBlock) void k_walk_row(const int32_t* __restrict__
       for (uint32_t i = off[b] + threadIdx.x; i < off[b + 1]; i += kBlock) {
         const uint32_t w = ent[i];
         if (shift <= kP16MaxShift) {   // two 16-bit entries per word (W = P here)
-          const uint32_t lo = w & 0xFFFFu, hi = w >> 16;
-          if (lo >> 13) atomicAdd(&acc[lo & 0x1FFFu], cx * static_cast<int>(lo >> 13));
-          if (hi >> 13) atomicAdd(&acc[hi & 0x1FFFu], cx * static_cast<int>(hi >> 13));
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const uint32_t h = (w >> (16 * half)) & 0xFFFFu;
+            const uint32_t e = h & 7u, lab = h >> 3;
+            if ((lab & 3u) == 3u && e >= 6u) continue;   // padding
+            atomicAdd(&acc[lab], cx << e);
+          }
           continue;
         }
         const uint32_t lab = w & 0xFFFFu;
@@ -455,10 +491,11 @@ int64_t dps_ct_tiles_ent_capacity(int64_t nnz, int64_t sum_c, int64_t n_mids,
   const int64_t T = (n_targets + tile_w - 1) / tile_w;
   const int64_t nb = n_mids * (T > 0 ? T : 1);
   if (log2_exact(tile_w) > kP16MaxShift) return nnz + 3 * (nb < nnz ? nb : nnz) + 4;
-  // 16-bit entries: ceil(c/7) <= 1 + (c-1)/7 pieces per C entry, up to 7
-  // padding entries per non-empty bucket, two entries per uint32 word
-  const int64_t pieces = nnz + (sum_c - nnz + kP16MaxC - 1) / kP16MaxC;
-  return (pieces + 7 * (nb < pieces ? nb : pieces) + 1) / 2 + 4;
+  // 16-bit entries: power-of-two pieces, at most (c + 1) / 2 <= 1 + (c - 1) / 2
+  // per C entry; up to 9 padding entries per non-empty bucket; two entries per
+  // uint32 word
+  const int64_t pieces = nnz + (sum_c - nnz + 1) / 2;
+  return (pieces + 9 * (nb < pieces ? nb : pieces) + 1) / 2 + 4;
 }
 
 size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t tile_w) {

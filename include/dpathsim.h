@@ -166,13 +166,16 @@ int dps_target_order(const int64_t* g, int64_t n_targets, int32_t key_bits,
  * into tiles of `tile_w` (power of two, 256..65536; the hot kernel keeps one
  * tile's packed u8 accumulators in LDS).  Bucket (v, t) holds, for every y of
  * tile t with C[y,v] > 0, packed entries in one of two formats:
- *   tile_w <= 8192: uint16 (c << 13) | (label(y) - t*tile_w), C[y,v] split into
- *                   ceil(C/7) pieces c <= 7 that sum to C[y,v];
+ *   tile_w <= 8192: uint16 (l << 3) | e, l = label(y) - t*tile_w, one piece
+ *                   of value 2^e; C[y,v] is split into power-of-two pieces that
+ *                   sum to it (e <= 7, and e <= 5 when l % 4 == 3: e = 6, 7 at
+ *                   l % 4 == 3 are padding codes);
  *   tile_w >= 16384: uint32 (C[y,v] << 16) | (label(y) - t*tile_w).
  * Buckets are stored contiguously in [v][t] order: bucket (v,t) is the uint32
  * words tile_ent[tile_off[v*T + t] .. tile_off[v*T + t + 1]),
- * T = ceil(n_targets/tile_w).  Every bucket is padded with C = 0 entries to 16
- * bytes, so bucket starts are 16-byte aligned and 16-byte chunks never straddle
+ * T = ceil(n_targets/tile_w).  Every bucket is padded to 16 bytes (32-bit:
+ * C = 0 entries; 16-bit: groups of padding codes {7,7} / {7,6,6} on one
+ * dword, which add C * 2^32 == 0 to packed u8 accumulators), so bucket starts are 16-byte aligned and 16-byte chunks never straddle
  * buckets.  tile_off uint32[n_mids*T + 1] (word offsets), tile_ent
  * uint32[dps_ct_tiles_ent_capacity()].
  * Optional: tile_maxc uint32[n_mids*T + 1] = max C[y,v] per bucket;
