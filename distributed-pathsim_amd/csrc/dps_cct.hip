@@ -406,7 +406,10 @@ __device__ __forceinline__ void scatter_u8(const Batch& B, uint32_t buf, uint32_
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const uint32_t c = static_cast<uint32_t>(B.c[u]);
-    if (c == 0) continue;   // dead chunk (beyond the stage's last)
+    // dead chunk (beyond the stage's last): skipped, although C = 0 would add
+    // nothing -- its lanes all point at entry 0, and 64 adds to one LDS dword
+    // serialise (branch-free: 115 -> 489 ms)
+    if (c == 0) continue;
     add_u8_word<P16>(buf, B.e[u].x, c, lab_mask);
     add_u8_word<P16>(buf, B.e[u].y, c, lab_mask);
     add_u8_word<P16>(buf, B.e[u].z, c, lab_mask);
