@@ -40,10 +40,12 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink authors/papers (debug)")
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--tile-w", type=int, default=8192)
+    ap.add_argument("--denominator", default="rowsum", choices=["rowsum", "diag"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01", "pmc_hot.json"),
-                    help="rocprofv3 PMC summary of the hot kernel (tools/pmc.sh) for roofline.traffic")
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r02", "pmc_hot.json"),
+                    help="rocprofv3 PMC summary of the hot kernel at HEAD (tools/pmc_hot.py): "
+                         "HBM bytes per launch (roofline.traffic) and VALU issue share")
     return ap.parse_args()
 
 
@@ -53,7 +55,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dpathsim.dist import balanced_bounds, gather_topk, max_shard
+    from dpathsim.dist import balanced_bounds, gather_topk, max_shard, pack_topk
     from dpathsim.engine import PathSimEngine
     from dpathsim.synth import CONFIGS, synth_config
 
@@ -79,27 +81,29 @@ def main():
     typed = graph.typed(__import__("dpathsim").METAPATHS[mp_name])
     NA = typed.n_authors
 
-    eng = PathSimEngine(typed, device=dev, tile_w=args.tile_w).upload()
+    eng = PathSimEngine(typed, device=dev, tile_w=args.tile_w,
+                        denominator=args.denominator).upload()
 
     def plan():
         # contiguous row shards of equal estimated work (every rank derives the
         # same bounds from its own, identical C: no communication)
         return balanced_bounds(eng.row_work(), world) if world > 1 else [(0, NA)]
 
-    eng.build()
+    eng.build()             # checks the overflow conditions once (one sync)
     bounds0 = plan()
     m = max_shard(NA, world, bounds0)
     out = (torch.empty((m, k), dtype=torch.int32, device=dev),
            torch.empty((m, k), dtype=torch.int64, device=dev),
            torch.empty((m, k), dtype=torch.float64, device=dev))
+    packed = torch.empty((m, 2 * k), dtype=torch.int64, device=dev)
     gathered = None
-    if world > 1:
-        gathered = tuple(torch.empty((world * m, k), dtype=t.dtype, device=dev) for t in out)
+    if world > 1 and rank == 0:
+        gathered = torch.empty((world * m, 2 * k), dtype=torch.int64, device=dev)
 
     ev_topk = []
 
     def step(record):
-        eng.build()
+        eng.build(check=False)   # no host read-back inside the step; checked after timing
         bounds = plan()
         if bounds != bounds0:
             raise RuntimeError("row shards changed between steps")
@@ -113,8 +117,9 @@ def main():
         if record:
             e1.record()
             ev_topk.append((e0, e1))
-        if world > 1:
-            gather_topk(out, NA, world, out=gathered, bounds=bounds)
+        if world > 1:   # one packed buffer per rank, gathered to rank 0 (RCCL)
+            pack_topk(*out, out=packed)
+            gather_topk(packed, NA, world, out=gathered, bounds=bounds)
 
     for _ in range(args.warmup):
         step(False)
@@ -130,6 +135,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    eng.check()              # the last step's overflow conditions (raises if violated)
     if world > 1:
         te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
@@ -139,6 +145,9 @@ def main():
     value = pairs / (elapsed / args.steps)
 
     # ---- roofline of the dominant kernel (dps_cct_topk), measured live --------
+    # algorithmic bytes per launch = bytes per C^T entry (16-bit entries up to
+    # tile_w 8192, 32-bit above) x sum_{x in shard} sum_{v in x} n_v entries
+    # read, + the top-k output (20 B per slot) + the row offsets
     topk_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_topk]))
     r0, r1 = bounds0[rank]
     shard = r1 - r0
@@ -149,23 +158,25 @@ def main():
     w = torch.zeros(nnz + 1, dtype=torch.int64, device=dev)
     w[1:] = torch.cumsum(n_v[c_col], 0)
     terms = int((w[c_ptr[r1]] - w[c_ptr[r0]]).item())      # sum_{x in shard} sum_{v in x} n_v
-    bytes_launch = 4 * terms + 20 * shard * k + 8 * (shard + 1)
+    ent_bytes = 2 if args.tile_w <= 8192 else 4
+    bytes_launch = ent_bytes * terms + 20 * shard * k + 8 * (shard + 1)
     achieved = bytes_launch / (topk_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, valu = None, None
     if args.pmc_json and os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
-            if (pm.get("config") == args.config and pm.get("world") == world
-                    and pm.get("tile_w", args.tile_w) == args.tile_w and args.scale == 1.0):
+            if (pm.get("config") == args.config and pm.get("world", 1) == world
+                    and pm.get("tile_w", args.tile_w) == args.tile_w and args.scale == 1.0
+                    and pm.get("k", k) == k and args.denominator == "rowsum"):
                 traffic = pm.get("hbm_bytes_per_launch")
+                valu = pm.get("valu")
         except Exception:
-            traffic = None
+            traffic, valu = None, None
     info = eng.info
 
     # ---- secondary rates the north star asks for -----------------------------
     # SpGEMM (C = W_AP . W_PV) against HBM: SURVEY §8d algorithmic bytes over the
-    # 'spgemm' phase of one extra timed build (events on the stream; the phase
-    # includes the two host size reads of the two-pass SpGEMM).
+    # 'spgemm' phase of one extra timed build (events on the stream).
     eng.build(timed=True)
     sp_ms = eng.info.phase_ms.get("spgemm", float("nan"))
     sp_bytes = (16 * (NA + 1) + 8 * eng.info.nnz_ap + 4 * typed.n_papers + 8 * eng.info.nnz_c)
@@ -173,14 +184,15 @@ def main():
               "achieved": sp_bytes / (sp_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     spgemm["frac"] = spgemm["achieved"] / HBM_PEAK_GBS
     # C.C^T against the dense int8 MFMA peak (5 POPS, MI355X_MICROARCH.md): the
-    # dense-equivalent rate (2 * rows * N_A * V padded to 64) and the intrinsic
-    # sparse rate (2 * sum_{x in shard} sum_{v in x} n_v multiply-adds).
+    # intrinsic sparse rate (2 * sum_{x in shard} sum_{v in x} n_v multiply-adds)
+    # as a fraction of that peak, and -- as a rate, not a fraction -- the
+    # dense-equivalent ops/s (2 * rows * N_A * V padded to 64) the all-pairs
+    # product would need on MFMA to finish in the same time.
     v_pad = (typed.n_mids + 63) // 64 * 64
-    dense_ops = 2.0 * shard * NA * v_pad
     cct = {"mfma_int8_dense_peak_ops": 5.0e15,
-           "dense_equiv_ops_per_s": dense_ops / (topk_ms * 1e-3),
-           "intrinsic_ops_per_s": 2.0 * terms / (topk_ms * 1e-3)}
-    cct["dense_equiv_frac_of_mfma_peak"] = cct["dense_equiv_ops_per_s"] / 5.0e15
+           "intrinsic_ops_per_s": 2.0 * terms / (topk_ms * 1e-3),
+           "dense_equiv_ops_per_s": 2.0 * shard * NA * v_pad / (topk_ms * 1e-3)}
+    cct["intrinsic_frac_of_mfma_int8_peak"] = cct["intrinsic_ops_per_s"] / 5.0e15
 
     # ---- CPU baseline: the oracle's C port on a bounded row sample ----------
     cpu = None
@@ -222,6 +234,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int32+f64",
+            "denominator": args.denominator,
             "data": "synthetic (dpathsim.synth, seed 20180417; dblp_large.gexf is absent)",
             "config": {"workload": f"{args.config}: synthetic DBLP {mp_name} "
                                    f"{NA} authors / {typed.n_papers} papers / "
@@ -229,10 +242,13 @@ def main():
                        "n_authors": NA, "k": k, "tile_w": args.tile_w,
                        "nnz_C": info.nnz_c, "sum_terms": terms if world == 1 else None,
                        "parallelism": f"row-shard x{world} (work-balanced, heaviest rows first)"},
-            "roofline": {"bound": "hbm", "kernel": "dps_cct_topk", "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "algorithmic_bytes": bytes_launch,
-                         "avg_launch_ms": topk_ms},
+            # bound: the resource that binds per the HEAD counters (VALU issue,
+            # see DESIGN.md §5); achieved/peak/frac: algorithmic bytes vs HBM
+            "roofline": {"bound": "valu" if valu else "hbm", "kernel": "dps_cct_topk",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes": bytes_launch, "bytes_per_entry": ent_bytes,
+                         "avg_launch_ms": topk_ms, "valu_issue": valu},
             "cpu_baseline": cpu,
             "phases_ms": {"cct_topk": topk_ms, "rest_of_step": ms_per_step - topk_ms},
             "spgemm_roofline": spgemm,

@@ -169,8 +169,8 @@ struct CctParams {
   double* out_score;
   unsigned long long* counter;
   bool dbuf;                 // two alternating stage buffers (W <= 16384) or one
-  int ablate;                // profiling aid (DPATHSIM_ABLATE): 1 no LDS adds, 2 no
-                             // candidate scoring, 4 no scatter
+  int ablate;                // profiling aid (DPATHSIM_ABLATE, -DDPS_PROFILE builds only):
+                             // 1 no LDS adds, 2 no candidate scoring, 4 no scatter
 };
 
 // Up to 64 venues of the row for one tile (lane j = venue g0 + j).
@@ -521,7 +521,7 @@ __device__ __forceinline__ void epilogue_u8(const CctParams& p, uint32_t* acc, T
   const int qd = nbuf / NW;
   const int end = (wave + 1) * qd;
   const int64_t tile_base = S.t << p.shift;
-  const bool score = (p.ablate & 2) == 0;
+  const bool score = !kProfile || (p.ablate & 2) == 0;
   const int64_t xr64 = x_lab - tile_base;
   const int xrel = (xr64 >= 0 && xr64 < (int64_t(1) << p.shift)) ? static_cast<int>(xr64) : -64;
   // one iteration: the 16-byte block of each lane (1024 targets, one segment)
@@ -627,7 +627,7 @@ __device__ __forceinline__ void epilogue(const CctParams& p, uint32_t* acc, TopK
   const uint32_t vmask = lnp == 2 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
   const int64_t tile_base = S.t << p.shift;
   const int pass_base = S.pass << (p.shift - lnp);
-  const bool score = (p.ablate & 2) == 0;
+  const bool score = !kProfile || (p.ablate & 2) == 0;
   for (int b0 = wave * qd; b0 < end; b0 += kWave * 4) {
     const int b = b0 + lane * 4;
     uint4 a = make_uint4(0, 0, 0, 0);
@@ -733,8 +733,8 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
   const int nbuf = 1 << (p.shift - 2);        // accumulator dwords per stage buffer
   // threshold segments of min(1024, W/4) targets: one epilogue iteration each
   const int seg_shift = p.shift - 2 < 10 ? p.shift - 2 : 10;
-  const bool no_add = (p.ablate & 1) != 0;
-  const bool no_scatter = (p.ablate & 4) != 0;
+  const bool no_add = kProfile && (p.ablate & 1) != 0;
+  const bool no_scatter = kProfile && (p.ablate & 4) != 0;
   CandQ Q;
   Q.lab = reinterpret_cast<int*>(lds + acc_dw) + wave * 2 * kQ;
   Q.m = Q.lab + kQ;
@@ -1085,7 +1085,10 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   p.out_idx = out_idx; p.out_cnt = out_cnt; p.out_score = out_score;
   p.counter = static_cast<unsigned long long*>(ws);
   p.ablate = 0;
-  if (const char* ab = std::getenv("DPATHSIM_ABLATE")) p.ablate = std::atoi(ab);
+  // Profiling aid only: the production build ignores DPATHSIM_ABLATE (an
+  // ablated run returns wrong top-k lists), the -DDPS_PROFILE build honours it.
+  if (kProfile)
+    if (const char* ab = std::getenv("DPATHSIM_ABLATE")) p.ablate = std::atoi(ab);
   DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : sizeof(unsigned long long), st));
   if (shift <= 13) return dispatch<true>(p, nw, k, st);   // 16-bit tile entries
   return dispatch<false>(p, nw, k, st);

@@ -89,57 +89,50 @@ class DPathSim_APVPA:
             return 0
         return self.dblp_graphframe.pairwise_walk(a, b)
 
+    def _emit(self, line, to_stdout=True):
+        if to_stdout:
+            print(line)
+        self.output_file.write(line + "\n")
+
     def run(self):
-        """DPathSim_APVPA.py:28-68: same prints and log lines, device-computed values."""
+        """DPathSim_APVPA.py:28-68: same prints and log lines, device-computed values.
+
+        The whole source row (pairwise walks, the targets' global walks and the
+        scores) is computed on the device up front; the loop below only formats."""
         eng = self.dblp_graphframe
         src = self.source_author_node_id
-        source_author_global_walk = self.metapath_global_walk(src)
-
-        print("Source author global walk: {}".format(source_author_global_walk))
-        self.output_file.write("Source author global walk: {}\n".format(source_author_global_walk))
+        gx = self.metapath_global_walk(src)
+        self._emit("Source author global walk: {}".format(gx))
 
         si = self.dblp_graph.index_of(src)
         na = eng.n_targets
-        if si is None:
-            m_row = torch.zeros(na, dtype=torch.int64, device=eng.device)
-        else:
-            m_row = eng.walk_row(si)
-        g = eng.tensor("g")[:na]
-        scores = torch.empty(max(na, 1), dtype=torch.float64, device=eng.device)
-        zero_div = torch.zeros(1, dtype=torch.int64, device=eng.device)
+        walks = (torch.zeros(na, dtype=torch.int64, device=eng.device) if si is None
+                 else eng.walk_row(si))
+        g_dev = eng.tensor("g")[:na]
+        sc_dev = torch.empty(max(na, 1), dtype=torch.float64, device=eng.device)
         with torch.cuda.device(eng.device):
-            _lib.call("dps_row_scores", m_row.data_ptr(), g.data_ptr(),
-                      int(source_author_global_walk), na, scores.data_ptr(), zero_div.data_ptr(),
-                      eng.stream)
-        m_h = m_row.cpu().tolist()
-        g_h = g.cpu().tolist()
-        s_h = scores[:na].cpu().tolist()
-        ordinal = {self.dblp_graph.node_id(n): o for o, n in enumerate(eng.typed.author_nodes.tolist())}
+            _lib.call("dps_row_scores", walks.data_ptr(), g_dev.data_ptr(), int(gx), na,
+                      sc_dev.data_ptr(), None, eng.stream)
+        walks_h, g_h, sc_h = walks.cpu().tolist(), g_dev.cpu().tolist(), sc_dev[:na].cpu().tolist()
+        ordinal_of = {self.dblp_graph.node_id(n): o
+                      for o, n in enumerate(eng.typed.author_nodes.tolist())}
+        names = self.author_id_name_maps
 
-        for target_author_node_id in self.author_sim_scores.keys():          # :36
-            start_time = timeit.default_timer()
-            o = ordinal[target_author_node_id]
-            pairwise_node_walk = int(m_h[o])
-            print("Pairwise authors walk {}: {}".format(target_author_node_id, pairwise_node_walk))
-            self.output_file.write("Pairwise authors walk {}: {}\n"
-                                   .format(target_author_node_id, pairwise_node_walk))
-            target_author_global_walk = int(g_h[o])
-            print("Target author global walk: {}".format(target_author_global_walk))
-            self.output_file.write("Target author global walk: {}\n"
-                                   .format(target_author_global_walk))
-            if source_author_global_walk + target_author_global_walk == 0:
-                raise ZeroDivisionError("division by zero")                   # :51-52
-            sim_score = s_h[o]
-            self.author_sim_scores.update({target_author_node_id: sim_score})
-            line = "Sim score {} - {}: {}".format(self.author_id_name_maps[src],   # :56 KeyError
-                                                   self.author_id_name_maps[target_author_node_id],
-                                                   sim_score)
-            print(line)
-            self.output_file.write(line + "\n")
-            self.output_file.write("***Stage done in: {}\n".format(timeit.default_timer() - start_time))
-            self.output_file.write("---\n")
+        for tgt in self.author_sim_scores.keys():                         # :36 target order
+            t_start = timeit.default_timer()
+            o = ordinal_of[tgt]
+            self._emit("Pairwise authors walk {}: {}".format(tgt, int(walks_h[o])))
+            gy = int(g_h[o])
+            self._emit("Target author global walk: {}".format(gy))
+            if gx + gy == 0:
+                raise ZeroDivisionError("division by zero")               # :51-52
+            self.author_sim_scores[tgt] = sc_h[o]
+            # names[src] raises KeyError for a non-author source, as :56 does
+            self._emit("Sim score {} - {}: {}".format(names[src], names[tgt], sc_h[o]))
+            self._emit("***Stage done in: {}".format(timeit.default_timer() - t_start), False)
+            self._emit("---", False)
             self.output_file.flush()
 
-        self.output_file.write("***Overall done in: {}\n"
-                               .format(timeit.default_timer() - self.overall_start_time))
+        self._emit("***Overall done in: {}".format(timeit.default_timer() - self.overall_start_time),
+                   False)
         self.output_file.close()

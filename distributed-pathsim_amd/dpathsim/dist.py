@@ -1,12 +1,23 @@
 """Row sharding of the all-pairs top-k across ranks.
 
 Every source row's top-k depends only on that row of C plus all of C and g,
-so ranks split the author rows into contiguous, balanced shards and exchange
-nothing but the finished top-k blocks.  One process per GPU; the collective is
-RCCL (``nccl`` backend) on the GPU box and gloo in the CPU tests.
+so ranks split the author rows into contiguous, work-balanced shards and
+exchange nothing but the finished top-k blocks.  One process per GPU; the
+collective is RCCL (``nccl`` backend) on the GPU box and gloo in the CPU tests.
+
+Results travel as ONE packed int64 buffer per rank, ``[rows, 2k]``: word 0..k-1
+holds (count << 32) | target index, word k..2k-1 the score's fp64 bits (16 B
+per entry; counts fit 32 bits because the engine checks max M[x,x] < 2^31 and
+M[x,y] <= max(M[x,x], M[y,y])).  They are gathered to rank 0 with a single
+``gather`` (not all-gathered to every rank), or written as per-rank shard files
+in row order when the result is too large for one host (config 5: 3M x top-100).
 """
 from __future__ import annotations
 
+import json
+import os
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -47,33 +58,98 @@ def balanced_bounds(work: torch.Tensor, world: int) -> list[tuple[int, int]]:
     return [(edges[r], edges[r + 1]) for r in range(world)]
 
 
-def gather_topk(parts, n_rows: int, world: int, group=None, out=None, bounds=None):
-    """All-gather every rank's top-k block into the full [n_rows, k] tensors.
+# ---------------------------------------------------------------- packing
+def pack_topk(idx: torch.Tensor, cnt: torch.Tensor, score: torch.Tensor, out=None):
+    """(idx int32, cnt int64, score f64) [R, k] -> int64 [R, 2k] (see module doc)."""
+    R, k = idx.shape
+    if out is None:
+        out = torch.empty((R, 2 * k), dtype=torch.int64, device=idx.device)
+    lo = idx.to(torch.int64) & 0xFFFFFFFF
+    out[:, :k] = (cnt.to(torch.int64) << 32) | lo
+    out[:, k:] = score.contiguous().view(torch.int64)
+    return out
+
+
+def unpack_topk(packed: torch.Tensor):
+    """Inverse of :func:`pack_topk`."""
+    k = packed.shape[1] // 2
+    w = packed[:, :k]
+    idx = (w & 0xFFFFFFFF).to(torch.int32)            # -1 round-trips through the low word
+    cnt = w >> 32
+    score = packed[:, k:].contiguous().view(torch.float64)
+    return idx, cnt, score
+
+
+def gather_topk(parts, n_rows: int, world: int, group=None, out=None, bounds=None, dst: int = 0):
+    """Gather every rank's top-k block to rank ``dst`` in ONE collective.
 
     ``parts``: this rank's (idx, cnt, score) tensors with shape [max_shard, k]
-    (rows past its shard are padding).  Returns (idx, cnt, score) for all
-    n_rows rows in row order on every rank; ``out`` may hold preallocated
-    [world * max_shard, k] receive buffers (reused across steps).  ``bounds``:
-    the shards in use (default: equal row counts, shard_bounds).
+    (rows past its shard are padding) -- or an already packed int64
+    [max_shard, 2k] tensor.  Returns (idx, cnt, score) for all n_rows rows in
+    row order on rank ``dst`` and None on the other ranks.  ``out``: an optional
+    preallocated receive buffer [world * max_shard, 2k] (int64) on ``dst``.
+    ``bounds``: the shards in use (default: equal row counts, shard_bounds).
     """
     if bounds is None:
         bounds = [shard_bounds(n_rows, r, world) for r in range(world)]
+    packed = parts if isinstance(parts, torch.Tensor) else pack_topk(*parts)
     if world == 1:
-        return tuple(p[:bounds[0][1]] for p in parts)
+        return unpack_topk(packed[:bounds[0][1] - bounds[0][0]])
     m = max_shard(n_rows, world, bounds)
-    if out is None:
-        out = tuple(torch.empty((world * m,) + tuple(p.shape[1:]), dtype=p.dtype, device=p.device)
-                    for p in parts)
-    for src, dst in zip(parts, out):
-        if src.shape[0] != m:
-            raise ValueError(f"part has {src.shape[0]} rows, expected max_shard {m}")
-        if dist.get_backend(group) == "nccl":
-            dist.all_gather_into_tensor(dst, src.contiguous(), group=group)
-        else:   # gloo (CPU tests, one-GPU rehearsal): host staging
-            host = dst.cpu() if dst.is_cuda else dst
-            dist.all_gather(list(host.view(world, m, *src.shape[1:]).unbind(0)),
-                            src.contiguous().cpu(), group=group)
-            if host is not dst:
-                dst.copy_(host)
-    rows = [slice(r * m, r * m + (b - a)) for r, (a, b) in enumerate(bounds)]
-    return tuple(torch.cat([o[s] for s in rows]) for o in out)
+    if packed.shape[0] != m:
+        raise ValueError(f"part has {packed.shape[0]} rows, expected max_shard {m}")
+    rank = dist.get_rank(group)
+    nccl = dist.get_backend(group) == "nccl"
+    src = packed.contiguous() if nccl else packed.contiguous().cpu()
+    recv = None
+    if rank == dst:
+        if out is None or not nccl:
+            out = torch.empty((world * m, packed.shape[1]), dtype=torch.int64,
+                              device=src.device)
+        recv = list(out.view(world, m, packed.shape[1]).unbind(0))
+    dist.gather(src, gather_list=recv, dst=dst, group=group)
+    if rank != dst:
+        return None
+    rows = [out[r * m: r * m + (b - a)] for r, (a, b) in enumerate(bounds)]
+    full = torch.cat(rows)
+    if full.device != packed.device:
+        full = full.to(packed.device)
+    return unpack_topk(full)
+
+
+# ------------------------------------------------------- per-rank shard files
+def write_topk_shard(directory, rank: int, world: int, bounds, parts, k: int) -> str:
+    """Write this rank's rows [r0, r1) as ``topk_rank{rank:05d}.npy`` (packed int64
+    [r1-r0, 2k]) plus a JSON manifest entry -- the per-rank output the survey
+    asks for when one gathered result would not fit a host."""
+    os.makedirs(directory, exist_ok=True)
+    r0, r1 = bounds[rank]
+    packed = parts if isinstance(parts, torch.Tensor) else pack_topk(*parts)
+    arr = packed[: r1 - r0].cpu().numpy()
+    path = os.path.join(directory, f"topk_rank{rank:05d}.npy")
+    np.save(path, arr, allow_pickle=False)
+    with open(os.path.join(directory, f"topk_rank{rank:05d}.json"), "w") as f:
+        json.dump({"rank": rank, "world": world, "row_begin": r0, "row_end": r1, "k": k,
+                   "layout": "int64 [rows, 2k]: (cnt << 32) | idx, then f64 score bits"}, f)
+    return path
+
+
+def read_topk_shards(directory):
+    """Merge the shard files of :func:`write_topk_shard` in row order (host tensors)."""
+    metas = []
+    for name in sorted(os.listdir(directory)):
+        if name.startswith("topk_rank") and name.endswith(".json"):
+            with open(os.path.join(directory, name)) as f:
+                metas.append(json.load(f))
+    if not metas:
+        raise FileNotFoundError(f"no topk shards in {directory}")
+    metas.sort(key=lambda m: m["row_begin"])
+    world = metas[0]["world"]
+    if len(metas) != world:
+        raise ValueError(f"{len(metas)} shard files for world {world}")
+    for a, b in zip(metas, metas[1:]):
+        if a["row_end"] != b["row_begin"]:
+            raise ValueError("shards do not tile the rows")
+    blocks = [np.load(os.path.join(directory, f"topk_rank{m['rank']:05d}.npy"), allow_pickle=False)
+              for m in metas]
+    return unpack_topk(torch.from_numpy(np.concatenate(blocks)))

@@ -40,10 +40,30 @@ class BuildInfo:
     phase_ms: dict = field(default_factory=dict)
 
 
-class PathSimEngine:
-    """All device state for one graph + meta-path on one GPU."""
+@dataclass
+class Bounds:
+    """Host-side capacity bounds, computed once from the raw (not yet distinct)
+    typed edge list at upload, so that build() never reads a size back from the
+    device: every count after distinct() is at most its raw-edge count."""
+    expand: int = 1      # >= sum_{x author} sum_{p in AP[x]} |PX[p]| (SpGEMM expansion)
+    sum_c: int = 1       # >= sum of C over all AP rows (>= sum of s)
+    key_bits: int = 1    # >= bit length of max g (and of max M[x,x])
 
-    def __init__(self, typed: TypedTables, device=None, tile_w: int = DEFAULT_TILE_W):
+
+DENOMINATORS = ("rowsum", "diag")
+
+
+class PathSimEngine:
+    """All device state for one graph + meta-path on one GPU.
+
+    ``denominator``: ``'rowsum'`` (default) is the reference's global walk
+    g[x] = sum_y M[x,y] (DPathSim_APVPA.py:70-88); ``'diag'`` is the
+    textbook PathSim M[x,x] + M[y,y].  It only changes which per-author term the
+    top-k kernel adds in the score's denominator.
+    """
+
+    def __init__(self, typed: TypedTables, device=None, tile_w: int = DEFAULT_TILE_W,
+                 denominator: str = "rowsum"):
         if not torch.cuda.is_available():
             raise RuntimeError("PathSimEngine needs a ROCm GPU (torch.cuda.is_available() is False);"
                                " there is no CPU fallback")
@@ -52,10 +72,15 @@ class PathSimEngine:
         self.device = torch.device(device if device is not None else "cuda")
         if tile_w & (tile_w - 1) or not 256 <= tile_w <= 65536:
             raise ValueError("tile_w must be a power of two in [256, 65536]")
+        if denominator not in DENOMINATORS:
+            raise ValueError(f"denominator must be one of {DENOMINATORS}")
         self.tile_w = int(tile_w)
+        self.denominator = denominator
         self.tile_skip = True
         self.info = BuildInfo()
+        self.bounds = None
         self.built = False
+        self.checked = False
         self._dev = {}
 
     # ------------------------------------------------------------------ utils
@@ -71,7 +96,8 @@ class PathSimEngine:
 
     # ----------------------------------------------------------------- upload
     def upload(self):
-        """Host -> HBM copy of the typed node tables and the raw edge list."""
+        """Host -> HBM copy of the typed node tables and the raw edge list, plus
+        the host-side capacity bounds (:class:`Bounds`)."""
         t = self.typed
         g = t.graph
         with torch.cuda.device(self.device):
@@ -84,19 +110,27 @@ class PathSimEngine:
                 node_rowid=to(t.node_rowid if g.n_nodes else np.zeros(1, np.int32)),
                 node_colid=to(t.node_colid if g.n_nodes else np.zeros(1, np.int32)),
             )
+        self.bounds = host_bounds(t)
         return self
 
     # ------------------------------------------------------------------ build
-    def build(self, timed: bool = False):
-        """Run the device build.  Inputs must be uploaded (resident in HBM)."""
+    def build(self, timed: bool = False, check: bool = True):
+        """Run the device build.  Inputs must be uploaded (resident in HBM).
+
+        Nothing is read back while the work is enqueued: buffers are sized from
+        :class:`Bounds`.  The overflow conditions (max C, max M[x,x], max g) are
+        checked by :meth:`check` -- here when ``check`` (one synchronisation at
+        the end), else by the caller before it trusts the results."""
         if "edge_src" not in self._dev:
             self.upload()
         t = self.typed
         d = self._dev
         st = self.stream
+        bnd = self.bounds
         N, E = t.graph.n_nodes, t.graph.n_edges
         NA, NP, NV = t.n_authors, t.n_papers, t.n_mids
         info = self.info = BuildInfo(n_nodes=N, n_edges=E, n_authors=NA, n_papers=NP, n_mids=NV)
+        self.checked = False
         marks = []
 
         def mark(name):
@@ -131,18 +165,15 @@ class PathSimEngine:
                       _ptr(px_col), _ptr(px_nnz), _ptr(ws), ws.numel(), st)
             del ap_r, ap_c, px_r, px_c
             mark("csr")
-            # A3: SpGEMM C = W_AP . W_PX over author rows [0, NA)
-            e_tot = self._empty(1, torch.int64)
-            _lib.call("dps_spgemm_expand_size", _ptr(ap_ptr), _ptr(ap_col), None, NA, _ptr(px_ptr),
-                      _ptr(e_tot), st)
-            expand = int(e_tot.item())                       # sync 1: size the workspace
+            # A3: SpGEMM C = W_AP . W_PX over author rows [0, NA); capacities from
+            # the raw-edge bound (expand >= nnz C), no size read-back
+            expand = bnd.expand
             sws = self._ws(_lib.size("dps_spgemm_workspace_size", NA, expand))
             c_ptr, c_nnz = self._empty(NA + 1, torch.int64), self._empty(2, torch.int64)
             _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, NA, _ptr(px_ptr),
                       _ptr(px_col), NP, _ptr(c_ptr), None, None, _ptr(c_nnz), expand, _ptr(sws),
                       sws.numel(), st)
-            nnz_c = int(c_nnz[0].item())                     # sync 2: allocate C
-            c_col, c_val = self._empty(nnz_c, torch.int32), self._empty(nnz_c, torch.int32)
+            c_col, c_val = self._empty(expand, torch.int32), self._empty(expand, torch.int32)
             _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, NA, _ptr(px_ptr),
                       _ptr(px_col), NP, _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(c_nnz),
                       expand, _ptr(sws), sws.numel(), st)
@@ -159,13 +190,14 @@ class PathSimEngine:
             _lib.call("dps_global_walks", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NA, _ptr(s),
                       _ptr(g), _ptr(diag), _ptr(stats), st)
             mark("walks")
-            host = torch.cat([stats, ap_nnz, px_nnz, s.sum().view(1)]).cpu()   # sync 3: stats
-            max_g = int(host[_lib.STAT_MAX_G])
-            # A5 operand layout: targets relabeled by ascending g, then tiled C^T
+            # the per-author denominator term of the score
+            den = g if self.denominator == "rowsum" else diag
+            # A5 operand layout: targets relabeled by ascending denominator term,
+            # then tiled C^T
             t_perm, t_rank = self._empty(NA, torch.int32), self._empty(NA, torch.int32)
             g_t = self._empty(NA, torch.int64)
             ows = self._ws(_lib.size("dps_target_order_workspace_size", NA))
-            _lib.call("dps_target_order", _ptr(g), NA, max(1, max_g.bit_length()), _ptr(t_perm),
+            _lib.call("dps_target_order", _ptr(den), NA, bnd.key_bits, _ptr(t_perm),
                       _ptr(t_rank), _ptr(g_t), _ptr(ows), ows.numel(), st)
             del ows
             mark("order")
@@ -173,44 +205,64 @@ class PathSimEngine:
             tile_off = self._empty(NV * T + 1, torch.int32)
             tile_maxc = self._empty(NV * T + 1, torch.int32)
             tile_gmin = self._empty(T, torch.int64)
-            sum_s = int(host[_lib.STATS_LEN + 2])   # >= sum of C's values (s covers every AP row)
-            ent_cap = _lib.size("dps_ct_tiles_ent_capacity", nnz_c, max(sum_s, nnz_c), NV, NA,
-                                self.tile_w)
+            ent_cap = _lib.size("dps_ct_tiles_ent_capacity", expand, max(bnd.sum_c, expand), NV,
+                                NA, self.tile_w)
             if ent_cap >= 2 ** 32:
                 raise OverflowError("padded nnz(C) >= 2^32 exceeds the uint32 tile offsets")
             tile_ent = self._empty(ent_cap, torch.int32)
             status = self._empty(1, torch.int32)
             tws = self._ws(_lib.size("dps_ct_tiles_workspace_size", NV, NA, self.tile_w))
-            _lib.call("dps_ct_tiles_build", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(g),
+            _lib.call("dps_ct_tiles_build", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(den),
                       _ptr(t_rank), NA, NV, self.tile_w, _ptr(tile_off), _ptr(tile_ent),
                       _ptr(tile_maxc), _ptr(tile_gmin), _ptr(status), _ptr(tws), tws.numel(), st)
             mark("tiles")
-            status_h = int(status.item())                          # sync 4
             del tws
         info.expand = expand
-        info.nnz_c = nnz_c
+        d.pop("row_work", None)
+        d.update(ap_ptr=ap_ptr, ap_col=ap_col, px_ptr=px_ptr, px_col=px_col, c_ptr=c_ptr,
+                 c_col=c_col, c_val=c_val, c_nnz=c_nnz, s=s, g=g, diag=diag, den=den, g_t=g_t,
+                 t_perm=t_perm, t_rank=t_rank, tile_off=tile_off, tile_ent=tile_ent,
+                 tile_maxc=tile_maxc, tile_gmin=tile_gmin, stats=stats, status=status,
+                 ap_nnz=ap_nnz, px_nnz=px_nnz,
+                 topk_ws=self._ws(_lib.size("dps_cct_topk_workspace_size")))
+        self.built = True
+        if timed:
+            torch.cuda.synchronize(self.device)
+            for (a, ea), (b, eb) in zip(marks, marks[1:]):
+                info.phase_ms[b] = ea.elapsed_time(eb)
+        if check:
+            self.check()
+        return self
+
+    def check(self):
+        """Read the build's statistics back (one synchronisation) and raise if a
+        value exceeds the engine's integer widths.  Fills ``info``."""
+        if not self.built:
+            raise RuntimeError("call build() first")
+        d = self._dev
+        info = self.info
+        host = torch.cat([d["stats"], d["ap_nnz"], d["px_nnz"], d["c_nnz"][:1],
+                          d["status"].to(torch.int64)]).cpu()
+        L = _lib.STATS_LEN
         info.max_c = int(host[_lib.STAT_MAX_C])
         info.max_diag = int(host[_lib.STAT_MAX_DIAG])
         info.max_g = int(host[_lib.STAT_MAX_G])
-        info.nnz_ap = int(host[_lib.STATS_LEN])
-        info.nnz_px = int(host[_lib.STATS_LEN + 1])
+        info.nnz_ap = int(host[L])
+        info.nnz_px = int(host[L + 1])
+        info.nnz_c = int(host[L + 2])
+        status_h = int(host[L + 3])
+        if info.nnz_c > self.bounds.expand:   # impossible by construction (raw >= distinct)
+            raise RuntimeError(f"nnz(C) {info.nnz_c} exceeds its bound {self.bounds.expand}")
         if status_h != 0 or info.max_c > 0xFFFF:
             raise OverflowError(f"max C[x,v] = {info.max_c} exceeds the 16-bit tile packing")
         if info.max_diag >= 2 ** 31:
             raise OverflowError(f"max M[x,x] = {info.max_diag} exceeds the int32 accumulators")
         if info.max_g >= 2 ** 52:
             raise OverflowError("g exceeds 2^52: gx+gy would not be exact in fp64")
-        if timed:
-            torch.cuda.synchronize(self.device)
-            for (a, ea), (b, eb) in zip(marks, marks[1:]):
-                info.phase_ms[b] = ea.elapsed_time(eb)
-        d.pop("row_work", None)
-        d.update(ap_ptr=ap_ptr, ap_col=ap_col, px_ptr=px_ptr, px_col=px_col, c_ptr=c_ptr,
-                 c_col=c_col, c_val=c_val, s=s, g=g, diag=diag, g_t=g_t, t_perm=t_perm,
-                 t_rank=t_rank, tile_off=tile_off, tile_ent=tile_ent, tile_maxc=tile_maxc,
-                 tile_gmin=tile_gmin, topk_ws=self._ws(_lib.size("dps_cct_topk_workspace_size")))
-        self.built = True
-        return self
+        if max(info.max_g, info.max_diag).bit_length() > self.bounds.key_bits:
+            raise RuntimeError("target-order key bound too small")   # impossible by construction
+        self.checked = True
+        return info
 
     # ------------------------------------------------------------- accessors
     def tensor(self, name):
@@ -227,13 +279,17 @@ class PathSimEngine:
         first and to balance row shards across ranks."""
         if "row_work" not in self._dev:
             d = self._dev
-            NA, nnz = self.typed.n_authors, self.info.nnz_c
+            NA, cap = self.typed.n_authors, d["c_col"].numel()
             with torch.cuda.device(self.device):
-                col = d["c_col"][:nnz].long()
-                n_v = torch.bincount(col, minlength=self.typed.n_mids)
-                pre = torch.zeros(nnz + 1, dtype=torch.int64, device=self.device)
-                pre[1:] = torch.cumsum(n_v[col], 0)
+                # n_v = nnz of column v (scatter-add over the valid prefix of c_col;
+                # no bincount, whose output size would need a host read-back)
                 ptr = d["c_ptr"][:NA + 1]
+                valid = torch.arange(cap, device=self.device) < ptr[-1]
+                col = d["c_col"].long().clamp_(0, max(self.typed.n_mids - 1, 0))
+                n_v = torch.zeros(max(self.typed.n_mids, 1), dtype=torch.int64, device=self.device)
+                n_v.scatter_add_(0, col, valid.to(torch.int64))
+                pre = torch.zeros(cap + 1, dtype=torch.int64, device=self.device)
+                pre[1:] = torch.cumsum(n_v[col] * valid, 0)
                 terms = pre[ptr[1:]] - pre[ptr[:-1]]
                 d["row_work"] = terms + (terms.sum() // max(NA, 1)) // 2
         return self._dev["row_work"]
@@ -267,7 +323,7 @@ class PathSimEngine:
                 w = self.row_work()[row_begin:row_end]
                 order = (torch.argsort(w, descending=True, stable=True) + row_begin).to(torch.int32)
             _lib.call("dps_cct_topk", _ptr(d["c_ptr"]), _ptr(d["c_col"]), _ptr(d["c_val"]),
-                      _ptr(d["g"]), _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA,
+                      _ptr(d["den"]), _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA,
                       self.typed.n_mids, self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
                       _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]),
                       int(row_begin), int(row_end), _ptr(order), int(k),
@@ -337,9 +393,39 @@ class PathSimEngine:
             return int(out.item())
 
 
-def build_engine(typed: TypedTables, device=None, tile_w=DEFAULT_TILE_W, timed=False):
+def host_bounds(typed: TypedTables) -> Bounds:
+    """Capacity bounds from the raw typed edges (see :class:`Bounds`)."""
+    from . import _lib as L
+    g = typed.graph
+    NA, NP, NV = typed.n_authors, typed.n_papers, typed.n_mids
+    if g.n_edges == 0 or NP == 0:
+        return Bounds()
+    src, dst, rel = g.edge_src, g.edge_dst, typed.edge_rel
+    nt = typed.node_type
+    ap = (rel == L.R_AP) & (nt[dst] == L.T_PAPER)
+    px = (rel == L.R_PX) & (nt[src] == L.T_PAPER) & (nt[dst] == L.T_MID)
+    col = typed.node_colid
+    ap_p = col[dst[ap]].astype(np.int64)
+    ap_row = typed.node_rowid[src[ap]].astype(np.int64)
+    px_p, px_v = col[src[px]].astype(np.int64), col[dst[px]].astype(np.int64)
+    pxdeg = np.bincount(px_p, minlength=NP)
+    per_edge = pxdeg[ap_p]                                   # raw |PX[p]| per raw AP edge
+    is_author = ap_row < NA
+    expand = int(per_edge[is_author].sum())
+    sum_c = int(per_edge.sum())
+    indeg = np.bincount(ap_p, minlength=NP)
+    s_max = int(np.bincount(px_v, weights=indeg[px_p], minlength=max(NV, 1)).max()) if len(px_v) else 0
+    row_c = np.bincount(ap_row[is_author], weights=per_edge[is_author], minlength=max(NA, 1))
+    c_row_max = int(row_c.max()) if NA else 0
+    # g[x] <= (sum_v C[x,v]) * max_v s_v;  M[x,x] <= (sum_v C[x,v])^2 <= that too
+    gb = max(c_row_max * max(s_max, c_row_max), 1)
+    return Bounds(expand=max(expand, 1), sum_c=max(sum_c, 1), key_bits=min(64, gb.bit_length()))
+
+
+def build_engine(typed: TypedTables, device=None, tile_w=DEFAULT_TILE_W, timed=False,
+                 denominator="rowsum"):
     t0 = time.perf_counter()
-    eng = PathSimEngine(typed, device=device, tile_w=tile_w).upload()
+    eng = PathSimEngine(typed, device=device, tile_w=tile_w, denominator=denominator).upload()
     eng.build(timed=timed)
     eng.info.phase_ms["host_total"] = (time.perf_counter() - t0) * 1e3
     return eng

@@ -160,7 +160,10 @@ def read_gexf(path, with_stats=False):
                     continue
                 key = (int(src[j]), int(dst[j]), kid)
                 if key in seen:
-                    rel[seen[key]] = rel[j]
+                    # networkx MultiGraph.add_edge does datadict.update(attr): a
+                    # repeat without a label keeps the earlier one
+                    if rel[j] is not KeyError:
+                        rel[seen[key]] = rel[j]
                     keep[j] = False
                 else:
                     seen[key] = j

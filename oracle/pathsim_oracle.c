@@ -28,6 +28,7 @@ typedef struct {
   int64_t *t_ptr;  /* CSC of C (author rows only) */
   int32_t *t_row, *t_val;
   int64_t *s, *g;
+  int64_t *diag;   /* M[x,x] = sum_v C[x,v]^2 (the textbook PathSim denominator term) */
 } orc_state;
 
 static int cmp_pair(const void* a, const void* b) {
@@ -119,6 +120,13 @@ orc_state* orc_create(int64_t n_ap, const int32_t* ap_row, const int32_t* ap_col
       gx += (int64_t)st->c_val[j] * st->s[st->c_col[j]];
     st->g[a] = gx;
   }
+  st->diag = (int64_t*)calloc((size_t)n_authors + 1, sizeof(int64_t));
+  for (int64_t a = 0; a < n_authors; ++a) {
+    int64_t dx = 0;
+    for (int64_t j = st->c_ptr[a]; j < st->c_ptr[a + 1]; ++j)
+      dx += (int64_t)st->c_val[j] * st->c_val[j];
+    st->diag[a] = dx;
+  }
   /* CSC of C (rows ascending within each column) */
   st->t_ptr = (int64_t*)calloc((size_t)n_mids + 1, sizeof(int64_t));
   for (int64_t j = 0; j < nnz; ++j) st->t_ptr[st->c_col[j] + 1]++;
@@ -153,9 +161,14 @@ static int better(double s1, int32_t y1, double s2, int32_t y2) {
   return s1 > s2 || (s1 == s2 && y1 < y2);
 }
 
-void orc_topk(const orc_state* st, int64_t row_begin, int64_t row_end, int k, int32_t* out_idx,
-              int64_t* out_cnt, double* out_score, int nthreads) {
+/* Top-k of source rows: rows[i] (i < n_rows) if rows != NULL, else row_begin + i.
+ * use_diag != 0 replaces the reference's row-sum denominator g[x] + g[y]
+ * (DPathSim_APVPA.py:51-52 with :70-88) by the textbook M[x,x] + M[y,y]. */
+void orc_topk_rows(const orc_state* st, const int64_t* rows, int64_t n_rows, int64_t row_begin,
+                   int k, int32_t* out_idx, int64_t* out_cnt, double* out_score, int nthreads,
+                   int use_diag) {
   const int64_t na = st->n_authors;
+  const int64_t* den_of = use_diag ? st->diag : st->g;
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
@@ -167,7 +180,8 @@ void orc_topk(const orc_state* st, int64_t row_begin, int64_t row_end, int k, in
     int32_t* ty = (int32_t*)malloc(sizeof(int32_t) * (size_t)k);
     int64_t* tm = (int64_t*)malloc(sizeof(int64_t) * (size_t)k);
 #pragma omp for schedule(dynamic, 16)
-    for (int64_t x = row_begin; x < row_end; ++x) {
+    for (int64_t i = 0; i < n_rows; ++i) {
+      const int64_t x = rows ? rows[i] : row_begin + i;
       int64_t nt = 0;
       for (int64_t j = st->c_ptr[x]; j < st->c_ptr[x + 1]; ++j) {
         const int32_t v = st->c_col[j];
@@ -179,13 +193,13 @@ void orc_topk(const orc_state* st, int64_t row_begin, int64_t row_end, int k, in
         }
       }
       int filled = 0;
-      const int64_t gx = st->g[x];
-      for (int64_t i = 0; i < nt; ++i) {
-        const int32_t y = touched[i];
+      const int64_t dx = den_of[x];
+      for (int64_t t = 0; t < nt; ++t) {
+        const int32_t y = touched[t];
         const int64_t m = acc[y];
         acc[y] = 0;
         if (y == x) continue;
-        const int64_t den = gx + st->g[y];
+        const int64_t den = dx + den_of[y];
         const double sc = den ? (double)(2 * m) / (double)den : 0.0;
         if (filled == k && !better(sc, y, ts[k - 1], ty[k - 1])) continue;
         int pos = filled < k ? filled : k - 1;
@@ -205,7 +219,7 @@ void orc_topk(const orc_state* st, int64_t row_begin, int64_t row_end, int k, in
         if (dup) continue;
         ts[filled] = 0.0; ty[filled] = (int32_t)y; tm[filled] = 0; ++filled;
       }
-      const int64_t o = (x - row_begin) * k;
+      const int64_t o = i * k;
       for (int q = 0; q < k; ++q) {
         if (q < filled) {
           out_idx[o + q] = ty[q]; out_cnt[o + q] = tm[q]; out_score[o + q] = ts[q];
@@ -218,10 +232,20 @@ void orc_topk(const orc_state* st, int64_t row_begin, int64_t row_end, int k, in
   }
 }
 
+void orc_topk(const orc_state* st, int64_t row_begin, int64_t row_end, int k, int32_t* out_idx,
+              int64_t* out_cnt, double* out_score, int nthreads) {
+  orc_topk_rows(st, NULL, row_end - row_begin, row_begin, k, out_idx, out_cnt, out_score,
+                nthreads, 0);
+}
+
+void orc_diag(const orc_state* st, int64_t* diag) {
+  memcpy(diag, st->diag, sizeof(int64_t) * (size_t)st->n_authors);
+}
+
 void orc_destroy(orc_state* st) {
   if (!st) return;
   free(st->c_ptr); free(st->c_col); free(st->c_val);
   free(st->t_ptr); free(st->t_row); free(st->t_val);
-  free(st->s); free(st->g);
+  free(st->s); free(st->g); free(st->diag);
   free(st);
 }

@@ -155,8 +155,12 @@ def scores_fp64(m, gx, gy):
     return out
 
 
-def allpairs_topk(graph: OracleGraph, k: int, rows=None, block: int = 512):
+def allpairs_topk(graph: OracleGraph, k: int, rows=None, block: int = 512,
+                  denominator: str = "rowsum"):
     """Top-k per author source by (score desc, author ordinal asc), self excluded.
+
+    ``denominator='rowsum'`` is the reference's 2M/(g[x]+g[y]) (K2); ``'diag'``
+    the textbook 2M/(M[x,x]+M[y,y]) that the CLI offers as an option.
 
     Returns (idx int32[R,k], cnt int64[R,k], score f64[R,k]); slots beyond the
     number of available targets hold idx -1, cnt 0, score 0.0.
@@ -169,7 +173,12 @@ def allpairs_topk(graph: OracleGraph, k: int, rows=None, block: int = 512):
     idx = np.full((R, k), -1, dtype=np.int32)
     cnt = np.zeros((R, k), dtype=np.int64)
     sc = np.zeros((R, k), dtype=np.float64)
-    g = graph.g
+    if denominator == "rowsum":
+        g = graph.g
+    elif denominator == "diag":
+        g = np.asarray(graph.C.multiply(graph.C).sum(axis=1)).ravel().astype(np.int64)
+    else:
+        raise ValueError(denominator)
     ar = np.arange(na)
     for b0 in range(0, R, block):
         rb = rows[b0:b0 + block]
@@ -226,6 +235,8 @@ class COracle:
         lib.orc_nnz.argtypes = [P]
         lib.orc_export.argtypes = [P, P, P, P, P, P]
         lib.orc_topk.argtypes = [P, I64, I64, C.c_int, P, P, P, C.c_int]
+        lib.orc_topk_rows.argtypes = [P, P, I64, I64, C.c_int, P, P, P, C.c_int, C.c_int]
+        lib.orc_diag.argtypes = [P, P]
         lib.orc_destroy.argtypes = [P]
         self._lib = lib
         a = [np.ascontiguousarray(x, dtype=np.int32) for x in (ap_row, ap_col, px_paper, px_mid)]
@@ -266,6 +277,28 @@ class COracle:
         self._lib.orc_topk(self._st, row_begin, row_end, k, idx.ctypes.data, cnt.ctypes.data,
                            sc.ctypes.data, int(threads))
         return idx, cnt, sc
+
+    def topk_rows(self, k, rows, threads=0, denominator="rowsum"):
+        """Top-k of the author rows listed in ``rows`` (any order, output row i is
+        rows[i]); ``denominator='diag'`` scores 2M/(M[x,x]+M[y,y]) instead of the
+        reference's row sums."""
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        R = len(rows)
+        idx = np.zeros((R, k), np.int32)
+        cnt = np.zeros((R, k), np.int64)
+        sc = np.zeros((R, k), np.float64)
+        if denominator not in ("rowsum", "diag"):
+            raise ValueError(denominator)
+        if R:
+            self._lib.orc_topk_rows(self._st, rows.ctypes.data, R, 0, k, idx.ctypes.data,
+                                    cnt.ctypes.data, sc.ctypes.data, int(threads),
+                                    int(denominator == "diag"))
+        return idx, cnt, sc
+
+    def diag(self):
+        d = np.zeros(max(self.n_authors, 1), np.int64)
+        self._lib.orc_diag(self._st, d.ctypes.data)
+        return d[: self.n_authors]
 
     def __del__(self):
         st = getattr(self, "_st", None)

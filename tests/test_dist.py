@@ -1,7 +1,9 @@
 """Multi-rank row sharding + top-k gather (dpathsim.dist) on CPU with gloo.
 
-The GPU path runs the same code with the nccl (RCCL) backend in bench.py; here
-the per-shard top-k comes from the C oracle so the test needs no GPU.
+The GPU path runs the same code with the nccl (RCCL) backend in bench.py.  The
+CPU tests here take each shard's top-k from the C oracle; the ``gpu``-marked
+test at the end computes the shards with the HIP engine (two gloo ranks on one
+GPU) and checks the gathered result against the oracle.
 """
 import os
 import socket
@@ -12,7 +14,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from dpathsim.dist import balanced_bounds, gather_topk, max_shard, shard_bounds
+from dpathsim.dist import (balanced_bounds, gather_topk, max_shard, pack_topk, read_topk_shards,
+                           shard_bounds, unpack_topk, write_topk_shard)
 
 
 @pytest.mark.parametrize("n", [0, 1, 7, 1000, 1_000_003])
@@ -68,11 +71,19 @@ def _worker(rank, world, port, k, result_path, balanced=False):
             p = torch.zeros((m, k), dtype=dt)
             p[: r1 - r0] = torch.from_numpy(a)
             parts.append(p)
-        gi, gc, gs = gather_topk(tuple(parts), na, world, bounds=bounds)
-        if rank == 0:
+        res = gather_topk(tuple(parts), na, world, bounds=bounds)
+        shard_dir = result_path + ".shards"
+        write_topk_shard(shard_dir, rank, world, bounds or [shard_bounds(na, r, world)
+                                                           for r in range(world)], tuple(parts), k)
+        dist.barrier()
+        if rank != 0:
+            assert res is None          # gathered to rank 0 only
+        else:
             fi, fc, fs = co.topk(k, 0, na, threads=1)
-            ok = (np.array_equal(gi.numpy(), fi) and np.array_equal(gc.numpy(), fc)
-                  and np.array_equal(gs.numpy().view(np.int64), fs.view(np.int64)))
+            ok = True
+            for gi, gc, gs in (res, read_topk_shards(shard_dir)):
+                ok = ok and (np.array_equal(gi.numpy(), fi) and np.array_equal(gc.numpy(), fc)
+                             and np.array_equal(gs.numpy().view(np.int64), fs.view(np.int64)))
             with open(result_path, "w") as f:
                 f.write("ok" if ok else "mismatch")
     finally:
@@ -84,5 +95,53 @@ def _worker(rank, world, port, k, result_path, balanced=False):
 def test_gloo_gather_equals_single_rank(tmp_path, world, balanced):
     out = tmp_path / "result.txt"
     mp.start_processes(_worker, args=(world, _free_port(), 10, str(out), balanced), nprocs=world,
+                       join=True, start_method="spawn")
+    assert out.read_text() == "ok"
+
+
+def test_pack_roundtrip():
+    rng = np.random.default_rng(0)
+    idx = torch.from_numpy(rng.integers(-1, 2 ** 31 - 1, (50, 7)).astype(np.int32))
+    cnt = torch.from_numpy(rng.integers(0, 2 ** 31 - 1, (50, 7)).astype(np.int64))
+    sc = torch.from_numpy(rng.random((50, 7)))
+    sc[0, 0] = 0.0
+    i2, c2, s2 = unpack_topk(pack_topk(idx, cnt, sc))
+    assert torch.equal(i2, idx) and torch.equal(c2, cnt)
+    assert torch.equal(s2.view(torch.int64), sc.view(torch.int64))
+
+
+def _engine_worker(rank, world, port, k, result_path):
+    """One rank of a 2-rank job on ONE GPU: its shard from the HIP engine."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pathsim_oracle as po
+        from dpathsim.engine import build_engine
+        from dpathsim.synth import synth_dblp
+        t = synth_dblp(6000, 18000, 300, seed=21).typed()
+        eng = build_engine(t, device="cuda:0", tile_w=1024)
+        na = t.n_authors
+        bounds = balanced_bounds(eng.row_work(), world)
+        r0, r1 = bounds[rank]
+        m = max_shard(na, world, bounds)
+        out = tuple(torch.zeros((m, k), dtype=dt, device=eng.device)
+                    for dt in (torch.int32, torch.int64, torch.float64))
+        eng.topk(k, r0, r1, out=tuple(o[: r1 - r0] for o in out))
+        res = gather_topk(out, na, world, bounds=bounds)
+        if rank == 0:
+            fi, fc, fs = po.COracle.from_typed(t).topk(k, 0, na)
+            gi, gc, gs = (a.cpu().numpy() for a in res)
+            ok = (np.array_equal(gi, fi) and np.array_equal(gc, fc)
+                  and np.array_equal(gs.view(np.int64), fs.view(np.int64)))
+            with open(result_path, "w") as f:
+                f.write("ok" if ok else "mismatch")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gloo_two_ranks_engine_shards(tmp_path):
+    out = tmp_path / "result.txt"
+    mp.start_processes(_engine_worker, args=(2, _free_port(), 10, str(out)), nprocs=2,
                        join=True, start_method="spawn")
     assert out.read_text() == "ok"

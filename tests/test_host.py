@@ -116,6 +116,40 @@ def test_gexf_multigraph_and_label_semantics(tmp_path):
     assert h.edges() == e
 
 
+def test_gexf_repeated_key_without_label_keeps_label(tmp_path):
+    """A repeated (u, v, id) edge without a label updates the edge's data dict
+    (networkx ``datadict.update``): the earlier label survives; an edge that
+    never gets a label raises KeyError('label') like the reference loop (:123-124)."""
+    head = """<?xml version='1.0' encoding='utf-8'?>
+<gexf version="1.2" xmlns="http://www.gexf.net/1.2draft">
+  <graph defaultedgetype="directed" mode="static">
+    <attributes class="edge" mode="static"><attribute id="1" title="label" type="string" />
+      <attribute id="2" title="w" type="string" /></attributes>
+    <attributes class="node" mode="static"><attribute id="0" title="node_type" type="string" /></attributes>
+    <nodes>
+      <node id="a" label="A"><attvalues><attvalue for="0" value="author" /></attvalues></node>
+      <node id="p" label="P"><attvalues><attvalue for="0" value="paper" /></attvalues></node>
+    </nodes>
+    <edges>
+"""
+    tail = "    </edges>\n  </graph>\n</gexf>"
+    ok = head + """      <edge id="7" source="a" target="p"><attvalues><attvalue for="1" value="author_of" /></attvalues></edge>
+      <edge id="7" source="a" target="p"><attvalues><attvalue for="2" value="x" /></attvalues></edge>
+""" + tail
+    p = tmp_path / "k.gexf"
+    p.write_text(ok)
+    v, e = _nx_tuples(str(p))
+    h = read_gexf(str(p))
+    assert h.edges() == e == [("a", "p", "author_of")]
+    bad = head + """      <edge id="7" source="a" target="p"><attvalues><attvalue for="2" value="x" /></attvalues></edge>
+""" + tail
+    p.write_text(bad)
+    with pytest.raises(KeyError):
+        _nx_tuples(str(p))
+    with pytest.raises(KeyError):
+        read_gexf(str(p))
+
+
 def test_synth_deterministic_and_shaped():
     a = synth_dblp(1000, 3000, 50, seed=9)
     b = synth_dblp(1000, 3000, 50, seed=9)
@@ -138,3 +172,41 @@ def test_c_abi_rejects_bad_arguments_without_gpu():
                           None, None, 0, 10, None, 0, None, None, None, None, 0, None)
     assert rc == _lib.DPS_ERR_UNSUPPORTED     # k = 0
     assert lib.dps_csr_build_workspace_size(100, 10) > 0
+
+
+def _raw_truth(typed):
+    """Exact post-distinct sizes from the C oracle (for the bound checks)."""
+    import pathsim_oracle as po
+    co = po.COracle.from_typed(typed)
+    cp, cc, cv, s, g = co.export()
+    return cp, cv, s, g, co.diag()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_host_bounds_dominate_device_sizes(seed, dblp_small_tuples):
+    """build() sizes every buffer from host_bounds (no device read-back): the
+    bounds must dominate nnz(C), sum(C), sum(s) and the bit length of max g."""
+    from dpathsim.engine import host_bounds
+    graphs = [synth_dblp(3000, 9000, 200, seed=seed),
+              synth_dblp(500, 3000, 50, seed=seed, mid_alpha=0.2, authors_lambda=6.0),
+              Graph.from_tuples(*dblp_small_tuples)]
+    for gr in graphs:
+        t = gr.typed()
+        b = host_bounds(t)
+        cp, cv, s, g, dg = _raw_truth(t)
+        assert b.expand >= cp[-1] and b.expand >= int(cv.sum())
+        assert b.sum_c >= int(s.sum())
+        assert b.key_bits >= max(int(g.max(initial=0)), int(dg.max(initial=0))).bit_length()
+
+
+def test_cli_arguments():
+    from dpathsim.cli import parse
+    a = parse(["--synth", "config3", "--all-pairs", "--topk", "10", "--denominator", "diag"])
+    assert a.all_pairs and a.denominator == "diag" and a.topk == 10
+    a = parse(["--graph", "g.gexf", "--source-name", "Jiawei Han"])
+    assert a.source_name == "Jiawei Han" and a.denominator == "rowsum"
+    for bad in (["--graph", "g"], ["--graph", "g", "--source-name", "x", "--denominator", "diag"],
+                ["--synth", "config3", "--all-pairs", "--topk", "0"],
+                ["--graph", "g", "--synth", "config3", "--all-pairs"]):
+        with pytest.raises(SystemExit):
+            parse(bad)

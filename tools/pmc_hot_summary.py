@@ -1,0 +1,57 @@
+"""Summarise tools/pmc_hot.sh passes into one JSON record for bench.py.
+
+hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (KiB counters;
+on gfx950 FETCH_SIZE reports half the bytes of wide 16-B/lane reads, which is
+how the kernel reads its C^T chunks -- MI355X_MICROARCH.md, HBM).
+valu.issue_frac = SQ_INSTS_VALU * 4 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8): wave
+instructions at one per 4 cycles per SIMD over the kernel's cycles (GRBM sums
+the 8 XCDs); valu.active_frac = SQ_ACTIVE_INST_VALU * 4 / (SQ_BUSY_CYCLES ...)
+is reported raw for cross-checking.
+usage: pmc_hot_summary.py DIR OUT_JSON
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def read(d, kernel="k_cct_topk"):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True)
+    tot = defaultdict(float)
+    disp = set()
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if kernel in row.get("Kernel_Name", ""):
+                tot[row["Counter_Name"]] += float(row["Counter_Value"])
+                disp.add(row.get("Dispatch_Id") or row.get("Correlation_Id"))
+    n = max(len(disp), 1)
+    return {k: v / n for k, v in tot.items()}, len(disp)
+
+
+base = sys.argv[1]
+c = {}
+for p in ("fetch", "write", "valu", "lds"):
+    d = os.path.join(base, f"pmc_{p}")
+    if os.path.isdir(d):
+        vals, n = read(d)
+        c.update({f"{k}@{p}" if k == "GRBM_GUI_ACTIVE" else k: v for k, v in vals.items()})
+rec = {"kernel": "k_cct_topk", "config": "config3", "world": 1, "tile_w": 8192, "k": 10,
+       "rows": int(os.environ.get("HOT_ROWS", "1000000")), "counters_per_launch": c}
+if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+    rec["hbm_bytes_per_launch"] = 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
+    rec["rule"] = "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950: FETCH_SIZE = half of 16-B/lane reads)"
+g = c.get("GRBM_GUI_ACTIVE@valu")
+if g and "SQ_INSTS_VALU" in c:
+    cyc = g / 8.0
+    rec["valu"] = {"insts_per_launch": c["SQ_INSTS_VALU"],
+                   "issue_frac": c["SQ_INSTS_VALU"] * 4.0 / (1024.0 * cyc),
+                   "kernel_cycles": cyc,
+                   "rule": "SQ_INSTS_VALU*4 / (1024 SIMDs * GRBM_GUI_ACTIVE/8)"}
+gl = c.get("GRBM_GUI_ACTIVE@lds")
+if "SQ_LDS_IDX_ACTIVE" in c:
+    rec["lds"] = {"bank_conflict_share": c.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(c["SQ_LDS_IDX_ACTIVE"], 1.0),
+                  "idx_active_per_cu_cycle": (c["SQ_LDS_IDX_ACTIVE"] / 256.0 / (gl / 8.0)) if gl else None}
+json.dump(rec, open(sys.argv[2], "w"), indent=1)
+print(json.dumps(rec))
