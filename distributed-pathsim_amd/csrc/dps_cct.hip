@@ -748,9 +748,11 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
     if (r >= p.n_rows) break;
     const int64_t x = p.row_order ? static_cast<int64_t>(p.row_order[r]) : p.row_begin + r;
     const int64_t ro = x - p.row_begin;   // output row
+    DPS_DASSERT(ro >= 0 && ro < p.n_rows);
     const int64_t x_lab = p.t_rank ? static_cast<int64_t>(p.t_rank[x]) : x;
     const int64_t pb = p.c_ptr[x];
     const int d = static_cast<int>(p.c_ptr[x + 1] - pb);
+    DPS_DASSERT(d >= 0);
     const int64_t gx = p.g[x];
     TopK<KPL> top;
     top.init(p.k);

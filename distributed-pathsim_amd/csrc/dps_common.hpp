@@ -7,11 +7,9 @@
 #include <cstddef>
 #include <cstdint>
 
-#include "dpathsim.h"
+#include "dps_host.hpp"
 
 namespace dps {
-
-void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 
 constexpr int kWave = 64;
 
@@ -177,12 +175,17 @@ hipError_t radix_sort_pairs(const uint64_t* keys_in, const uint32_t* vals_in, ui
     }                                                                                  \
   } while (0)
 
-#define DPS_REQUIRE(cond, code, ...)                                                   \
-  do {                                                                                 \
-    if (!(cond)) {                                                                     \
-      dps::set_error(__VA_ARGS__);                                                     \
-      return (code);                                                                   \
-    }                                                                                  \
-  } while (0)
-
 #define DPS_LAUNCHED() DPS_HIP_RET(hipGetLastError())
+
+// Device asserts of the debug build (make debug: -DDPS_DEBUG): a failed check
+// traps the wave (the launch then reports an error); compiled out otherwise.
+#ifdef DPS_DEBUG
+#define DPS_DASSERT(cond)                                                              \
+  do {                                                                                 \
+    if (!(cond)) __builtin_trap();                                                     \
+  } while (0)
+#else
+#define DPS_DASSERT(cond) \
+  do {                    \
+  } while (0)
+#endif

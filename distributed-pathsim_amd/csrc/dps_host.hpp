@@ -1,0 +1,17 @@
+// Host-only error plumbing shared by every translation unit of libdpathsim
+// (no HIP headers: dps_log.cpp and the sanitizer builds use it alone).
+#pragma once
+
+#include "dpathsim.h"
+
+namespace dps {
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+}  // namespace dps
+
+#define DPS_REQUIRE(cond, code, ...)                                                   \
+  do {                                                                                 \
+    if (!(cond)) {                                                                     \
+      dps::set_error(__VA_ARGS__);                                                     \
+      return (code);                                                                   \
+    }                                                                                  \
+  } while (0)

@@ -24,7 +24,7 @@
 #include <thread>
 #include <vector>
 
-#include "dps_common.hpp"
+#include "dps_host.hpp"
 
 namespace dps {
 namespace {
