@@ -162,6 +162,7 @@ struct CctParams {
   int shift;
   int64_t row_begin;
   const int32_t* row_order;  // nullable: dequeue order of the rows (e.g. heaviest first)
+  bool out_by_slot;          // output row = dequeue slot (dps_cct_topk_rows), else x - row_begin
   int64_t n_rows;
   int k;
   int32_t* out_idx;
@@ -747,7 +748,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
     const int64_t r = row_s;
     if (r >= p.n_rows) break;
     const int64_t x = p.row_order ? static_cast<int64_t>(p.row_order[r]) : p.row_begin + r;
-    const int64_t ro = x - p.row_begin;   // output row
+    const int64_t ro = p.out_by_slot ? r : x - p.row_begin;   // output row
     DPS_DASSERT(ro >= 0 && ro < p.n_rows);
     const int64_t x_lab = p.t_rank ? static_cast<int64_t>(p.t_rank[x]) : x;
     const int64_t pb = p.c_ptr[x];
@@ -1039,21 +1040,18 @@ extern "C" {
 
 size_t dps_cct_topk_workspace_size(void) { return 256; }
 
-int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
-                 const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
-                 const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
-                 const uint32_t* tile_off, const uint32_t* tile_ent, const uint32_t* tile_maxc,
-                 const int64_t* tile_gmin, int64_t row_begin, int64_t row_end,
-                 const int32_t* row_order, int32_t k,
-                 int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
-                 size_t ws_bytes, void* stream) {
+static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                         const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
+                         const int32_t* t_rank, int64_t n_targets, int64_t n_mids,
+                         int32_t tile_w, const uint32_t* tile_off, const uint32_t* tile_ent,
+                         const uint32_t* tile_maxc, const int64_t* tile_gmin, int64_t row_begin,
+                         int64_t n_rows, const int32_t* row_order, bool out_by_slot, int32_t k,
+                         int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
+                         size_t ws_bytes, void* stream) {
   const int shift = log2_exact(tile_w);
   DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED,
               "tile_w must be a power of two in [256, 65536], got %d", tile_w);
   DPS_REQUIRE(k >= 1 && k <= 256, DPS_ERR_UNSUPPORTED, "k must be in [1, 256], got %d", k);
-  DPS_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= n_targets, DPS_ERR_INVALID,
-              "row range [%lld, %lld) outside [0, %lld)", static_cast<long long>(row_begin),
-              static_cast<long long>(row_end), static_cast<long long>(n_targets));
   DPS_REQUIRE(n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "n_targets exceeds int32");
   DPS_REQUIRE(n_mids * ((n_targets + tile_w - 1) / tile_w) < int64_t(UINT32_MAX), DPS_ERR_OVERFLOW,
               "n_mids * tiles exceeds the 32-bit bucket index");
@@ -1063,7 +1061,6 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   DPS_REQUIRE(ws && ws_bytes >= dps_cct_topk_workspace_size(), DPS_ERR_WORKSPACE,
               "cct_topk workspace too small");
   auto st = static_cast<hipStream_t>(stream);
-  const int64_t n_rows = row_end - row_begin;
   if (n_rows == 0) return DPS_OK;
   CctParams p;
   p.c_ptr = c_ptr; p.c_col = c_col; p.c_val = c_val;
@@ -1083,7 +1080,8 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   DPS_REQUIRE(nw != 8 || shift > 13, DPS_ERR_INVALID, "8 waves per row need tile_w >= 16384");
 
   p.dbuf = nw > 1 && shift <= 14;   // 2 x W bytes of u8 accumulators up to W = 16384, one 32 KB buffer above
-  p.row_begin = row_begin; p.row_order = row_order; p.n_rows = n_rows; p.k = k;
+  p.row_begin = row_begin; p.row_order = row_order; p.out_by_slot = out_by_slot;
+  p.n_rows = n_rows; p.k = k;
   p.out_idx = out_idx; p.out_cnt = out_cnt; p.out_score = out_score;
   p.counter = static_cast<unsigned long long*>(ws);
   p.ablate = 0;
@@ -1094,6 +1092,37 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : sizeof(unsigned long long), st));
   if (shift <= 13) return dispatch<true>(p, nw, k, st);   // 16-bit tile entries
   return dispatch<false>(p, nw, k, st);
+}
+
+int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                 const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
+                 const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                 const uint32_t* tile_off, const uint32_t* tile_ent, const uint32_t* tile_maxc,
+                 const int64_t* tile_gmin, int64_t row_begin, int64_t row_end,
+                 const int32_t* row_order, int32_t k,
+                 int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
+                 size_t ws_bytes, void* stream) {
+  DPS_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= n_targets, DPS_ERR_INVALID,
+              "row range [%lld, %lld) outside [0, %lld)", static_cast<long long>(row_begin),
+              static_cast<long long>(row_end), static_cast<long long>(n_targets));
+  return cct_topk_impl(c_ptr, c_col, c_val, g, g_t, t_perm, t_rank, n_targets, n_mids, tile_w,
+                       tile_off, tile_ent, tile_maxc, tile_gmin, row_begin, row_end - row_begin,
+                       row_order, false, k, out_idx, out_cnt, out_score, ws, ws_bytes, stream);
+}
+
+int dps_cct_topk_rows(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                      const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
+                      const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                      const uint32_t* tile_off, const uint32_t* tile_ent,
+                      const uint32_t* tile_maxc, const int64_t* tile_gmin, const int32_t* rows,
+                      int64_t n_rows, int32_t k, int32_t* out_idx, int64_t* out_cnt,
+                      double* out_score, void* ws, size_t ws_bytes, void* stream) {
+  DPS_REQUIRE(n_rows >= 0 && n_rows <= n_targets, DPS_ERR_INVALID, "bad n_rows %lld",
+              static_cast<long long>(n_rows));
+  DPS_REQUIRE(n_rows == 0 || rows, DPS_ERR_INVALID, "rows is required");
+  return cct_topk_impl(c_ptr, c_col, c_val, g, g_t, t_perm, t_rank, n_targets, n_mids, tile_w,
+                       tile_off, tile_ent, tile_maxc, tile_gmin, 0, n_rows, rows, true, k,
+                       out_idx, out_cnt, out_score, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

@@ -120,6 +120,51 @@ __global__ __launch_bounds__(kBlock) void k_scatter_rows(
 
 // ---------------------------------------------------------------------------
 // Segmented sort + unique (+ run lengths).
+// Tiny segments (2..16): one lane each, a 16-input bitonic network in registers.
+constexpr int kLaneSeg = 16;
+
+__device__ __forceinline__ void lane_sort_unique(int32_t* __restrict__ data,
+                                                 int32_t* __restrict__ counts, int64_t beg,
+                                                 int len, int64_t* __restrict__ uniq_out) {
+  int32_t v[kLaneSeg];
+#pragma unroll
+  for (int i = 0; i < kLaneSeg; ++i) v[i] = i < len ? data[beg + i] : INT_MAX;
+#pragma unroll
+  for (int k = 2; k <= kLaneSeg; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+      for (int i = 0; i < kLaneSeg; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          const int32_t a = v[i], b = v[l];
+          const bool up = (i & k) == 0;
+          v[i] = up ? min(a, b) : max(a, b);
+          v[l] = up ? max(a, b) : min(a, b);
+        }
+      }
+    }
+  }
+  int u = 0;
+  int run = 0;
+#pragma unroll
+  for (int i = 0; i < kLaneSeg; ++i) {
+    if (i < len) {
+      const bool first = i == 0 || v[i] != v[i - 1];
+      if (first) {
+        if (i > 0 && counts) counts[beg + u - 1] = run;
+        data[beg + u] = v[i];
+        ++u;
+        run = 1;
+      } else {
+        ++run;
+      }
+    }
+  }
+  if (counts) counts[beg + u - 1] = run;
+  *uniq_out = u;
+}
+
 // Short segments (<= 64): one wave, bitonic sort in registers.
 __global__ __launch_bounds__(kBlock) void k_seg_short(int32_t* __restrict__ data,
                                                       int32_t* __restrict__ counts,
@@ -145,11 +190,13 @@ __global__ __launch_bounds__(kBlock) void k_seg_short(int32_t* __restrict__ data
       if (ll <= 1) {
         uniq[sl] = ll;
         if (ll == 1 && counts) counts[bl] = 1;
+      } else if (ll <= kLaneSeg) {
+        lane_sort_unique(data, counts, bl, ll, uniq + sl);
       } else if (ll > kWave) {
         long_list[atomicAdd(n_long, 1u)] = static_cast<int32_t>(sl);
       }
     }
-    uint64_t todo = ballot(ll >= 2 && ll <= kWave);
+    uint64_t todo = ballot(ll > kLaneSeg && ll <= kWave);
     while (todo) {
       const int src = __ffsll(static_cast<long long>(todo)) - 1;
       todo &= todo - 1;
@@ -398,25 +445,45 @@ __global__ __launch_bounds__(kBlock) void k_expand(const int64_t* __restrict__ a
                                                    const int32_t* __restrict__ px_col,
                                                    const int64_t* __restrict__ exp_ptr,
                                                    int32_t* __restrict__ tmp) {
+  // 64 output rows per wave: a lane expands its own row when the row has at
+  // most 32 papers (the common case), the whole wave expands longer rows
   const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
-  for (int64_t i = wave0; i < n_out; i += nwaves) {
-    const int64_t r = out_row_src(rows, i);
-    const int64_t b = ap_ptr[r], e = ap_ptr[r + 1];
-    int64_t out = exp_ptr[i];
-    for (int64_t c0 = b; c0 < e; c0 += kWave) {
-      const int64_t j = c0 + lane;
-      int64_t pb = 0, pl = 0;
-      if (j < e) {
-        const int32_t p = ap_col[j];
-        pb = px_ptr[p];
-        pl = px_ptr[p + 1] - pb;
+  for (int64_t i0 = wave0 * kWave; i0 < n_out; i0 += nwaves * kWave) {
+    const int64_t i = i0 + lane;
+    int64_t b = 0, e = 0, out = 0;
+    if (i < n_out) {
+      const int64_t r = out_row_src(rows, i);
+      b = ap_ptr[r];
+      e = ap_ptr[r + 1];
+      out = exp_ptr[i];
+      if (e - b <= 32) {
+        for (int64_t j = b; j < e; ++j) {
+          const int32_t p = ap_col[j];
+          for (int64_t t = px_ptr[p]; t < px_ptr[p + 1]; ++t) tmp[out++] = px_col[t];
+        }
       }
-      const int64_t inc = wave_inclusive_sum(pl);
-      int64_t o = out + inc - pl;
-      for (int64_t t = 0; t < pl; ++t) tmp[o + t] = px_col[pb + t];
-      out += readlane(inc, kWave - 1);
+    }
+    uint64_t todo = ballot(e - b > 32);
+    while (todo) {
+      const int l = __ffsll(static_cast<long long>(todo)) - 1;
+      todo &= todo - 1;
+      const int64_t bb = readlane(b, l), ee = readlane(e, l);
+      int64_t o = readlane(out, l);
+      for (int64_t c0 = bb; c0 < ee; c0 += kWave) {
+        const int64_t j = c0 + lane;
+        int64_t pb = 0, pl = 0;
+        if (j < ee) {
+          const int32_t p = ap_col[j];
+          pb = px_ptr[p];
+          pl = px_ptr[p + 1] - pb;
+        }
+        const int64_t inc = wave_inclusive_sum(pl);
+        int64_t w = o + inc - pl;
+        for (int64_t t = 0; t < pl; ++t) tmp[w + t] = px_col[pb + t];
+        o += readlane(inc, kWave - 1);
+      }
     }
   }
 }
@@ -525,6 +592,75 @@ __global__ __launch_bounds__(kBlock) void k_global_walks(const int64_t* __restri
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && stats)
     stats[DPS_STAT_NNZ_C] = static_cast<unsigned long long>(c_ptr[n_rows] - c_ptr[0]);
+}
+
+// Per-row work estimate of the hot kernel: terms[x] = sum_{v in x} n_v, n_v =
+// nnz of column v of C (over rows [0, n_rows)).  Column counts are reduced in
+// LDS per block (one global atomic per mid and block) when they fit.
+constexpr int64_t kColLds = 8192;
+
+__global__ __launch_bounds__(kBlock) void k_col_counts(const int64_t* __restrict__ c_ptr,
+                                                       const int32_t* __restrict__ c_col,
+                                                       int64_t n_rows, int64_t n_mids,
+                                                       unsigned* __restrict__ n_v) {
+  // block (x, y) counts the mids [y*kColLds, (y+1)*kColLds) of its share of the
+  // entries in LDS: hot (heavy) mids never take one global atomic per entry
+  __shared__ unsigned h[kColLds];
+  const int64_t m0 = static_cast<int64_t>(blockIdx.y) * kColLds;
+  const int64_t m1 = min(m0 + kColLds, n_mids);
+  for (int64_t i = threadIdx.x; i < m1 - m0; i += kBlock) h[i] = 0;
+  __syncthreads();
+  const int64_t nnz = c_ptr[n_rows] - c_ptr[0];
+  for (int64_t j = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; j < nnz;
+       j += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int64_t v = c_col[c_ptr[0] + j];
+    if (v >= m0 && v < m1) atomicAdd(&h[v - m0], 1u);
+  }
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < m1 - m0; i += kBlock)
+    if (h[i]) atomicAdd(&n_v[m0 + i], h[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_row_terms(const int64_t* __restrict__ c_ptr,
+                                                      const int32_t* __restrict__ c_col,
+                                                      int64_t n_rows,
+                                                      const unsigned* __restrict__ n_v,
+                                                      int64_t* __restrict__ terms) {
+  for (int64_t x = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; x < n_rows;
+       x += static_cast<int64_t>(gridDim.x) * kBlock) {
+    int64_t t = 0;
+    for (int64_t j = c_ptr[x]; j < c_ptr[x + 1]; ++j) t += n_v[c_col[j]];
+    terms[x] = t;
+  }
+}
+
+// s[v] = sum over rows [0, n_rows) of C[r,v] (column sums of C over every AP
+// row = the mid walks of the global-walk motif): per-block LDS sums, one
+// global atomic per mid and block when the mids fit in LDS.
+constexpr int64_t kSumLds = 6144;
+
+__global__ __launch_bounds__(kBlock) void k_col_sums(const int64_t* __restrict__ c_ptr,
+                                                     const int32_t* __restrict__ c_col,
+                                                     const int32_t* __restrict__ c_val,
+                                                     int64_t n_rows, int64_t n_mids,
+                                                     unsigned long long* __restrict__ s) {
+  // block (x, y) sums the mids [y*kSumLds, (y+1)*kSumLds) of its share of the
+  // entries in LDS, one global atomic per mid and block
+  __shared__ unsigned long long h[kSumLds];
+  const int64_t m0 = static_cast<int64_t>(blockIdx.y) * kSumLds;
+  const int64_t m1 = min(m0 + kSumLds, n_mids);
+  for (int64_t i = threadIdx.x; i < m1 - m0; i += kBlock) h[i] = 0;
+  __syncthreads();
+  const int64_t b0 = c_ptr[0], nnz = c_ptr[n_rows] - b0;
+  for (int64_t j = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; j < nnz;
+       j += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int64_t v = c_col[b0 + j];
+    if (v >= m0 && v < m1)
+      atomicAdd(&h[v - m0], static_cast<unsigned long long>(c_val[b0 + j]));
+  }
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < m1 - m0; i += kBlock)
+    if (h[i]) atomicAdd(&s[m0 + i], h[i]);
 }
 
 }  // namespace
@@ -709,7 +845,7 @@ int dps_spgemm_count(const int64_t* ap_ptr, const int32_t* ap_col, const int32_t
     }
     DPS_HIP_RET(scan_exclusive<int64_t>(e_len, exp_ptr, n_out_rows, sws, scan_ws, st));
     if (n_out_rows > 0) {
-      k_expand<<<grid_for(n_out_rows * kWave, kBlock), kBlock, 0, st>>>(
+      k_expand<<<grid_for(n_out_rows, kBlock), kBlock, 0, st>>>(
           ap_ptr, ap_col, rows, n_out_rows, px_ptr, px_col, exp_ptr, tmp);
       DPS_LAUNCHED();
     }
@@ -751,6 +887,40 @@ int dps_global_walks(const int64_t* c_ptr, const int32_t* c_col, const int32_t* 
   if (stats) DPS_HIP_RET(hipMemsetAsync(stats, 0, DPS_STATS_LEN * sizeof(int64_t), st));
   k_global_walks<<<grid_for(n_rows, kBlock), kBlock, 0, st>>>(
       c_ptr, c_col, c_val, n_rows, s, g, diag, reinterpret_cast<unsigned long long*>(stats));
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+int dps_col_sums(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                 int64_t n_rows, int64_t n_mids, int64_t* s, void* stream) {
+  DPS_REQUIRE(n_rows >= 0 && n_mids >= 0, DPS_ERR_INVALID, "negative size");
+  DPS_REQUIRE(c_ptr && (n_mids == 0 || s), DPS_ERR_INVALID, "null array");
+  auto st = static_cast<hipStream_t>(stream);
+  if (n_mids == 0) return DPS_OK;
+  DPS_HIP_RET(hipMemsetAsync(s, 0, n_mids * sizeof(int64_t), st));
+  if (n_rows == 0) return DPS_OK;
+  const unsigned ny = static_cast<unsigned>((n_mids + kSumLds - 1) / kSumLds);
+  k_col_sums<<<dim3(ny > 1 ? 256 : 512, ny), kBlock, 0, st>>>(
+      c_ptr, c_col, c_val, n_rows, n_mids, reinterpret_cast<unsigned long long*>(s));
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+int dps_row_work(const int64_t* c_ptr, const int32_t* c_col, int64_t n_rows, int64_t n_mids,
+                 uint32_t* col_count_ws, int64_t* terms, void* stream) {
+  DPS_REQUIRE(n_rows >= 0 && n_mids >= 0, DPS_ERR_INVALID, "negative size");
+  DPS_REQUIRE(c_ptr && terms && (n_mids == 0 || col_count_ws), DPS_ERR_INVALID, "null array");
+  auto st = static_cast<hipStream_t>(stream);
+  if (n_rows == 0) return DPS_OK;
+  if (n_mids > 0) {
+    DPS_HIP_RET(hipMemsetAsync(col_count_ws, 0, n_mids * sizeof(uint32_t), st));
+    const unsigned ny = static_cast<unsigned>((n_mids + kColLds - 1) / kColLds);
+    k_col_counts<<<dim3(ny > 1 ? 128 : 256, ny), kBlock, 0, st>>>(c_ptr, c_col, n_rows, n_mids,
+                                                                  col_count_ws);
+    DPS_LAUNCHED();
+  }
+  k_row_terms<<<grid_for(n_rows, kBlock), kBlock, 0, st>>>(c_ptr, c_col, n_rows, col_count_ws,
+                                                          terms);
   DPS_LAUNCHED();
   return DPS_OK;
 }

@@ -16,6 +16,8 @@
 //                      reference's run() loop computes it (:30-52).
 #include "dps_common.hpp"
 
+#include <cstdlib>
+
 namespace dps {
 namespace {
 
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restri
 // range with one global atomicAdd per (block, venue) and places entries with
 // LDS cursors.  Entry order inside a bucket is unspecified either way.
 constexpr int kBlkMids = 8192;
-constexpr int kBlkLabels = 1024;
+constexpr int kBlkLabels = 4096;   // default labels per block (tools/build_ab.py: 1.08 ms vs 1.24 ms at 1024)
 // 16 waves per block (one 64-label group each): with 64 KB of LDS per block a
 // CU holds two blocks = 32 waves, enough to cover the latency of the gathers.
 constexpr int kBlkThreads = 1024;
@@ -449,10 +451,22 @@ int log2_exact(int32_t w) {
   return (1 << s) == w ? s : -1;
 }
 
+// Labels per block of the block-local build: a power of two in [1024, tile_w]
+// (DPATHSIM_TILE_LPB overrides the default, for A/B runs).  Every block writes
+// one count slot per (mid, part), so fewer, wider parts shrink the slot arrays
+// and their scan; more parts give more blocks.
+int tile_lpb(int32_t tile_w) {
+  int lpb = kBlkLabels;
+  if (const char* e = std::getenv("DPATHSIM_TILE_LPB")) lpb = std::atoi(e);
+  if (lpb < 1024 || (lpb & (lpb - 1))) lpb = kBlkLabels;
+  return tile_w < lpb ? tile_w : lpb;
+}
+
 // Parts per tile of the block-local build (1 on the global-atomic path).
 int64_t tile_parts(int64_t n_mids, int32_t tile_w) {
   if (n_mids > kBlkMids) return 1;
-  return tile_w > kBlkLabels ? tile_w / kBlkLabels : 1;
+  const int lpb = tile_lpb(tile_w);
+  return tile_w > lpb ? tile_w / lpb : 1;
 }
 
 }  // namespace
@@ -545,7 +559,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   uint32_t* mxp = c.take<uint32_t>(np + 1);
   int32_t* perm = c.take<int32_t>(n_targets > 0 ? n_targets : 1);
   DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "tiles workspace carve failed");
-  const int lpb = tile_w < kBlkLabels ? tile_w : kBlkLabels;
+  const int lpb = tile_lpb(tile_w);
   const int64_t nblk = (n_targets + lpb - 1) / lpb;
   const bool p16 = shift <= kP16MaxShift;   // counts and offsets are in entries
   const uint32_t per16 = p16 ? 8u : 4u;

@@ -45,6 +45,8 @@ SIGNATURES = {
                                    _i64, _p, _sz, _p]),
     "dps_mid_walks": (C.c_int, [_p, _p, _i64, _p, _p, _i64, _i64, _p, _p, _p]),
     "dps_global_walks": (C.c_int, [_p, _p, _p, _i64, _p, _p, _p, _p, _p]),
+    "dps_row_work": (C.c_int, [_p, _p, _i64, _i64, _p, _p, _p]),
+    "dps_col_sums": (C.c_int, [_p, _p, _p, _i64, _i64, _p, _p]),
     "dps_target_order_workspace_size": (_sz, [_i64]),
     "dps_target_order": (C.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "dps_ct_tiles_workspace_size": (_sz, [_i64, _i64, _i32]),
@@ -54,6 +56,8 @@ SIGNATURES = {
     "dps_cct_topk_workspace_size": (_sz, []),
     "dps_cct_topk": (C.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p,
                                _i64, _i64, _p, _i32, _p, _p, _p, _p, _sz, _p]),
+    "dps_cct_topk_rows": (C.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p,
+                                    _p, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "dps_walk_row": (C.c_int, [_p, _p, _i64, _p, _i64, _i64, _i32, _p, _p, _p, _p]),
     "dps_row_scores": (C.c_int, [_p, _p, _i64, _i64, _p, _p, _p]),
     "dps_pair_count": (C.c_int, [_p, _p, _i64, _p, _p, _i64, _p, _p]),

@@ -165,25 +165,25 @@ class PathSimEngine:
                       _ptr(px_col), _ptr(px_nnz), _ptr(ws), ws.numel(), st)
             del ap_r, ap_c, px_r, px_c
             mark("csr")
-            # A3: SpGEMM C = W_AP . W_PX over author rows [0, NA); capacities from
-            # the raw-edge bound (expand >= nnz C), no size read-back
-            expand = bnd.expand
-            sws = self._ws(_lib.size("dps_spgemm_workspace_size", NA, expand))
-            c_ptr, c_nnz = self._empty(NA + 1, torch.int64), self._empty(2, torch.int64)
-            _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, NA, _ptr(px_ptr),
+            # A3: SpGEMM C = W_AP . W_PX over EVERY AP row (author rows [0, NA)
+            # first, then untyped author_of sources): capacities from the raw-edge
+            # bound (expand >= nnz C), no size read-back
+            expand = bnd.sum_c
+            sws = self._ws(_lib.size("dps_spgemm_workspace_size", N, expand))
+            c_ptr, c_nnz = self._empty(N + 1, torch.int64), self._empty(2, torch.int64)
+            _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, N, _ptr(px_ptr),
                       _ptr(px_col), NP, _ptr(c_ptr), None, None, _ptr(c_nnz), expand, _ptr(sws),
                       sws.numel(), st)
             c_col, c_val = self._empty(expand, torch.int32), self._empty(expand, torch.int32)
-            _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, NA, _ptr(px_ptr),
+            _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, N, _ptr(px_ptr),
                       _ptr(px_col), NP, _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(c_nnz),
                       expand, _ptr(sws), sws.numel(), st)
             del sws
             mark("spgemm")
-            # A4: s (over ALL AP rows), g = C.s, diag, stats
+            # A4: s = column sums of C over ALL AP rows, g = C.s over author rows,
+            # diag, stats
             s = self._empty(NV, torch.int64)
-            indeg = self._empty(NP, torch.int32)
-            _lib.call("dps_mid_walks", _ptr(ap_ptr), _ptr(ap_col), N, _ptr(px_ptr), _ptr(px_col),
-                      NP, NV, _ptr(indeg), _ptr(s), st)
+            _lib.call("dps_col_sums", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), N, NV, _ptr(s), st)
             g = self._empty(NA, torch.int64)
             diag = self._empty(NA, torch.int64)
             stats = self._empty(_lib.STATS_LEN, torch.int64)
@@ -205,8 +205,8 @@ class PathSimEngine:
             tile_off = self._empty(NV * T + 1, torch.int32)
             tile_maxc = self._empty(NV * T + 1, torch.int32)
             tile_gmin = self._empty(T, torch.int64)
-            ent_cap = _lib.size("dps_ct_tiles_ent_capacity", expand, max(bnd.sum_c, expand), NV,
-                                NA, self.tile_w)
+            ent_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV, NA,
+                                self.tile_w)
             if ent_cap >= 2 ** 32:
                 raise OverflowError("padded nnz(C) >= 2^32 exceeds the uint32 tile offsets")
             tile_ent = self._empty(ent_cap, torch.int32)
@@ -217,7 +217,6 @@ class PathSimEngine:
                       _ptr(tile_maxc), _ptr(tile_gmin), _ptr(status), _ptr(tws), tws.numel(), st)
             mark("tiles")
             del tws
-        info.expand = expand
         d.pop("row_work", None)
         d.update(ap_ptr=ap_ptr, ap_col=ap_col, px_ptr=px_ptr, px_col=px_col, c_ptr=c_ptr,
                  c_col=c_col, c_val=c_val, c_nnz=c_nnz, s=s, g=g, diag=diag, den=den, g_t=g_t,
@@ -243,16 +242,18 @@ class PathSimEngine:
         info = self.info
         host = torch.cat([d["stats"], d["ap_nnz"], d["px_nnz"], d["c_nnz"][:1],
                           d["status"].to(torch.int64)]).cpu()
+        # nnz over the author rows (C also holds the untyped author_of rows)
         L = _lib.STATS_LEN
         info.max_c = int(host[_lib.STAT_MAX_C])
         info.max_diag = int(host[_lib.STAT_MAX_DIAG])
         info.max_g = int(host[_lib.STAT_MAX_G])
         info.nnz_ap = int(host[L])
         info.nnz_px = int(host[L + 1])
-        info.nnz_c = int(host[L + 2])
+        info.nnz_c = int(host[_lib.STAT_NNZ_C])
+        info.expand = int(host[L + 2])         # nnz of C over every AP row
         status_h = int(host[L + 3])
-        if info.nnz_c > self.bounds.expand:   # impossible by construction (raw >= distinct)
-            raise RuntimeError(f"nnz(C) {info.nnz_c} exceeds its bound {self.bounds.expand}")
+        if info.expand > self.bounds.sum_c:   # impossible by construction (raw >= distinct)
+            raise RuntimeError(f"nnz(C) {info.expand} exceeds its bound {self.bounds.sum_c}")
         if status_h != 0 or info.max_c > 0xFFFF:
             raise OverflowError(f"max C[x,v] = {info.max_c} exceeds the 16-bit tile packing")
         if info.max_diag >= 2 ** 31:
@@ -279,18 +280,13 @@ class PathSimEngine:
         first and to balance row shards across ranks."""
         if "row_work" not in self._dev:
             d = self._dev
-            NA, cap = self.typed.n_authors, d["c_col"].numel()
+            NA, NV = self.typed.n_authors, self.typed.n_mids
             with torch.cuda.device(self.device):
-                # n_v = nnz of column v (scatter-add over the valid prefix of c_col;
-                # no bincount, whose output size would need a host read-back)
-                ptr = d["c_ptr"][:NA + 1]
-                valid = torch.arange(cap, device=self.device) < ptr[-1]
-                col = d["c_col"].long().clamp_(0, max(self.typed.n_mids - 1, 0))
-                n_v = torch.zeros(max(self.typed.n_mids, 1), dtype=torch.int64, device=self.device)
-                n_v.scatter_add_(0, col, valid.to(torch.int64))
-                pre = torch.zeros(cap + 1, dtype=torch.int64, device=self.device)
-                pre[1:] = torch.cumsum(n_v[col] * valid, 0)
-                terms = pre[ptr[1:]] - pre[ptr[:-1]]
+                terms = self._empty(NA, torch.int64)
+                ncol = self._empty(NV, torch.int32)
+                _lib.call("dps_row_work", _ptr(d["c_ptr"]), _ptr(d["c_col"]), NA, NV, _ptr(ncol),
+                          _ptr(terms), self.stream)
+                terms = terms[:NA]
                 d["row_work"] = terms + (terms.sum() // max(NA, 1)) // 2
         return self._dev["row_work"]
 
@@ -331,33 +327,44 @@ class PathSimEngine:
                       self.stream)
         return idx, cnt, sc
 
+    def topk_rows(self, k: int, rows, out=None):
+        """★ top-k of an arbitrary list of author rows (device or host int array),
+        one launch, rows dequeued heaviest first; output row i is rows[i]."""
+        if not self.built:
+            raise RuntimeError("call build() first")
+        d = self._dev
+        NA = self.typed.n_authors
+        rows = torch.as_tensor(rows, device=self.device).to(torch.int64).reshape(-1)
+        R = rows.numel()
+        if out is None:
+            out = (torch.empty((R, k), dtype=torch.int32, device=self.device),
+                   torch.empty((R, k), dtype=torch.int64, device=self.device),
+                   torch.empty((R, k), dtype=torch.float64, device=self.device))
+        if R == 0:
+            return out
+        with torch.cuda.device(self.device):
+            perm = torch.argsort(self.row_work()[rows], descending=True, stable=True)
+            order = rows[perm].to(torch.int32)
+            tmp = tuple(torch.empty_like(o) for o in out)
+            _lib.call("dps_cct_topk_rows", _ptr(d["c_ptr"]), _ptr(d["c_col"]), _ptr(d["c_val"]),
+                      _ptr(d["den"]), _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA,
+                      self.typed.n_mids, self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
+                      _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]),
+                      _ptr(order), R, int(k), _ptr(tmp[0]), _ptr(tmp[1]), _ptr(tmp[2]),
+                      _ptr(d["topk_ws"]), d["topk_ws"].numel(), self.stream)
+            for o, t in zip(out, tmp):
+                o[perm] = t
+        return out
+
     # -------------------------------------------------------- single source
     def source_row(self, node_index: int):
-        """Sparse C row (cols, vals device tensors) of ANY node (DPathSim_APVPA.py:77)."""
+        """Sparse C row (cols, vals device tensors) of ANY node (DPathSim_APVPA.py:77):
+        C is built over every row id, so non-author sources of author_of edges
+        have their rows too (empty for nodes without such edges)."""
         d = self._dev
-        t = self.typed
-        rid = int(t.node_rowid[node_index])
-        if rid < t.n_authors:
-            b, e = (int(v) for v in d["c_ptr"][rid:rid + 2].cpu())
-            return d["c_col"][b:e], d["c_val"][b:e]
-        st = self.stream
-        with torch.cuda.device(self.device):
-            rows = torch.tensor([rid], dtype=torch.int32, device=self.device)
-            e_tot = self._empty(1, torch.int64)
-            _lib.call("dps_spgemm_expand_size", _ptr(d["ap_ptr"]), _ptr(d["ap_col"]), _ptr(rows),
-                      1, _ptr(d["px_ptr"]), _ptr(e_tot), st)
-            expand = int(e_tot.item())
-            ws = self._ws(_lib.size("dps_spgemm_workspace_size", 1, expand))
-            c_ptr, c_nnz = self._empty(2, torch.int64), self._empty(2, torch.int64)
-            _lib.call("dps_spgemm_count", _ptr(d["ap_ptr"]), _ptr(d["ap_col"]), _ptr(rows), 1,
-                      _ptr(d["px_ptr"]), _ptr(d["px_col"]), t.n_papers, _ptr(c_ptr), None, None,
-                      _ptr(c_nnz), expand, _ptr(ws), ws.numel(), st)
-            nnz = int(c_nnz[0].item())
-            col, val = self._empty(nnz, torch.int32), self._empty(nnz, torch.int32)
-            _lib.call("dps_spgemm_count", _ptr(d["ap_ptr"]), _ptr(d["ap_col"]), _ptr(rows), 1,
-                      _ptr(d["px_ptr"]), _ptr(d["px_col"]), t.n_papers, _ptr(c_ptr), _ptr(col),
-                      _ptr(val), _ptr(c_nnz), expand, _ptr(ws), ws.numel(), st)
-        return col[:nnz], val[:nnz]
+        rid = int(self.typed.node_rowid[node_index])
+        b, e = (int(v) for v in d["c_ptr"][rid:rid + 2].cpu())
+        return d["c_col"][b:e], d["c_val"][b:e]
 
     def global_walk(self, node_index: int) -> int:
         """metapath_global_walk (DPathSim_APVPA.py:70-88) for any node."""

@@ -147,6 +147,21 @@ int dps_mid_walks(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_ap_row
 int dps_global_walks(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
                      int64_t n_rows, const int64_t* s, int64_t* g, int64_t* diag,
                      int64_t* stats, void* stream);
+/* s from C itself: s[v] = sum_{r < n_rows} C[r,v] (int64[n_mids], written).
+ * With C built over EVERY AP row (authors and untyped author_of sources) this
+ * equals dps_mid_walks' s without the per-paper in-degree pass; the engine
+ * builds C that way. */
+int dps_col_sums(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                 int64_t n_rows, int64_t n_mids, int64_t* s, void* stream);
+
+/* Work estimate per source row of the hot kernel (used to order rows heaviest
+ * first and to balance row shards across ranks):
+ * terms[x] = sum_{v : C[x,v] > 0} n_v with n_v = nnz of column v over rows
+ * [0, n_rows) -- the C^T entries row x's scatter reads.  col_count_ws:
+ * uint32[n_mids] scratch (left holding n_v).  No reference counterpart (the
+ * reference has no work partitioning). */
+int dps_row_work(const int64_t* c_ptr, const int32_t* c_col, int64_t n_rows, int64_t n_mids,
+                 uint32_t* col_count_ws, int64_t* terms, void* stream);
 
 /* ---------------------------------------------------------------------------
  * A5 operand layout, step 1: target relabeling (a pure layout choice; results
@@ -224,6 +239,18 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
                  int64_t row_begin, int64_t row_end, const int32_t* row_order, int32_t k,
                  int32_t* out_idx, int64_t* out_cnt, double* out_score,
                  void* ws, size_t ws_bytes, void* stream);
+
+/* The same for an arbitrary list of source rows (any order, repeats allowed):
+ * output row i is rows[i] (rows[i] in [0, n_targets)), and rows are dequeued
+ * in list order, so a caller passes them heaviest first.  Used for row-sampled
+ * parity runs and for non-contiguous shards. */
+int dps_cct_topk_rows(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                      const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
+                      const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                      const uint32_t* tile_off, const uint32_t* tile_ent,
+                      const uint32_t* tile_maxc, const int64_t* tile_gmin, const int32_t* rows,
+                      int64_t n_rows, int32_t k, int32_t* out_idx, int64_t* out_cnt,
+                      double* out_score, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Single-source row (the reference's run() loop, :30-50): for one sparse C row

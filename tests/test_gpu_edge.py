@@ -134,3 +134,20 @@ def test_config3_full_output_properties():
         assert cnt[x, s] == m
         want = np.float64(2 * m) / np.float64(int(g[x]) + int(g[y]))
         assert sc[x, s].view(np.int64) == want.view(np.int64)
+
+
+def test_topk_rows_matches_contiguous_launch():
+    """dps_cct_topk_rows (arbitrary row list, repeats allowed, heaviest-first
+    dequeue) gives the rows of the contiguous launch."""
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_dblp
+    t = synth_dblp(6000, 18000, 300, seed=13).typed()
+    eng = build_engine(t, tile_w=1024)
+    full = [a.cpu().numpy() for a in eng.topk(10)]
+    rng = np.random.default_rng(5)
+    rows = np.concatenate([rng.integers(0, t.n_authors, 700), [0, 5999, 17, 17]])
+    got = [a.cpu().numpy() for a in eng.topk_rows(10, rows)]
+    for a, b in zip(got, full):
+        assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
+                              (b.view(np.int64) if b.dtype == np.float64 else b)[rows])
+    assert all(a.shape[0] == 0 for a in eng.topk_rows(10, np.zeros(0, np.int64)))

@@ -36,21 +36,22 @@ def _cmp(got, want, rows=None):
                              f"orc {oi[bad[0]]} {oc[bad[0]]} {os_[bad[0]]}")
 
 
-def _topk_rows(eng, k, rows):
-    """Engine top-k of an arbitrary row list (one launch per contiguous run)."""
-    import torch
+def _oracle_rows(co, k, rows, chunk=256):
+    """C oracle top-k of a row list in chunks, printing progress (long oracle
+    runs must keep writing: the GPU box kills silent commands)."""
     rows = np.asarray(rows, dtype=np.int64)
-    out = [np.zeros((len(rows), k), dt) for dt in (np.int32, np.int64, np.float64)]
-    order = np.argsort(rows, kind="stable")
-    srt = rows[order]
-    cuts = np.flatnonzero(np.diff(srt) != 1) + 1
-    for seg in np.split(np.arange(len(srt)), cuts):
-        r0, r1 = int(srt[seg[0]]), int(srt[seg[-1]]) + 1
-        res = eng.topk(k, r0, r1)
-        for o, a in zip(out, res):
-            o[order[seg]] = a.cpu().numpy()
-    torch.cuda.synchronize()
-    return out
+    parts = []
+    t0 = time.perf_counter()
+    for i in range(0, len(rows), chunk):
+        parts.append(co.topk_rows(k, rows[i:i + chunk]))
+        print(f"  oracle rows {min(i + chunk, len(rows))}/{len(rows)} "
+              f"({time.perf_counter() - t0:.0f} s)", flush=True)
+    return tuple(np.concatenate([p[j] for p in parts]) for j in range(3))
+
+
+def _topk_rows(eng, k, rows):
+    """Engine top-k of an arbitrary row list (one dps_cct_topk_rows launch)."""
+    return [a.cpu().numpy() for a in eng.topk_rows(k, np.asarray(rows, dtype=np.int64))]
 
 
 def test_config3_all_rows_bench_shape():
@@ -61,7 +62,8 @@ def test_config3_all_rows_bench_shape():
     eng = build_engine(t, tile_w=8192)              # the bench configuration
     got = eng.topk(10)
     t0 = time.perf_counter()
-    want = po.COracle.from_typed(t).topk(10, 0, t.n_authors)
+    co = po.COracle.from_typed(t)
+    want = _oracle_rows(co, 10, np.arange(t.n_authors), chunk=100_000)
     print(f"oracle: all {t.n_authors} rows in {time.perf_counter() - t0:.1f} s")
     _cmp(got, want)
 
@@ -78,7 +80,7 @@ def test_config4_heaviest_and_wide_rows():
     rows = np.union1d(np.argsort(-work, kind="stable")[:5000], np.flatnonzero(d > 64))
     assert (d > 64).sum() > 0
     print(f"config4: {len(rows)} rows ({(d > 64).sum()} with > 64 topics)")
-    _cmp(_topk_rows(eng, 10, rows), po.COracle.from_typed(t).topk_rows(10, rows), rows)
+    _cmp(_topk_rows(eng, 10, rows), _oracle_rows(po.COracle.from_typed(t), 10, rows), rows)
 
 
 def _wide_bound_rows(eng, t, cap=3000):
@@ -116,7 +118,7 @@ def test_config5_heaviest_and_wide_bound_rows():
     assert len(wide) > 0
     rows = np.union1d(np.argsort(-work, kind="stable")[:2000], wide)
     print(f"config5: {len(rows)} rows ({len(wide)} with a tile bound > 255)")
-    _cmp(_topk_rows(eng, 100, rows), po.COracle.from_typed(t).topk_rows(100, rows), rows)
+    _cmp(_topk_rows(eng, 100, rows), _oracle_rows(po.COracle.from_typed(t), 100, rows), rows)
 
 
 def _crafted_wide_counts(n_fill=20000, seed=5):
@@ -190,4 +192,5 @@ def test_config2_standin_gexf_roundtrip(tmp_path):
     assert np.array_equal(h.node_type_idx, g.node_type_idx)
     t = h.typed()
     eng = build_engine(t)
-    _cmp(eng.topk(10), po.COracle.from_typed(t).topk(10, 0, t.n_authors))
+    _cmp(eng.topk(10), _oracle_rows(po.COracle.from_typed(t), 10, np.arange(t.n_authors),
+                                    chunk=20_000))

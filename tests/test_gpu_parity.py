@@ -19,7 +19,7 @@ def test_dblp_small_counts_bit_exact(small_engine, dblp_small_expected):
     ex = dblp_small_expected
     nnz = eng.info.nnz_c
     assert nnz == len(ex["c_col"])
-    assert np.array_equal(eng.tensor("c_ptr").cpu().numpy(), ex["c_ptr"])
+    assert np.array_equal(eng.tensor("c_ptr")[: len(ex["c_ptr"])].cpu().numpy(), ex["c_ptr"])
     assert np.array_equal(eng.tensor("c_col")[:nnz].cpu().numpy(), ex["c_col"])
     assert np.array_equal(eng.tensor("c_val")[:nnz].cpu().numpy(), ex["c_val"])
     assert np.array_equal(eng.tensor("s")[: len(ex["s"])].cpu().numpy(), ex["s"])
