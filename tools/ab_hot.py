@@ -45,6 +45,13 @@ for W in Ws:
         ms, _ = timed(eng, R)
         res[f"W{W}_ablate{ab}"] = ms
         print(f"  ablate {ab}: {ms:.1f} ms", flush=True)
+        if ab == "16":   # shader-clock cycles per phase, summed over waves
+            c = eng.tensor("topk_ws")[:256].view(torch.int64).cpu().tolist()
+            names = ["scatter", "flush", "barrier1", "find", "prefetch", "epilogue", "barrier2"]
+            st = max(c[15], 1)
+            print("  cycles per wave-stage: " + " ".join(f"{n} {c[8 + i] / st:.0f}"
+                                                         for i, n in enumerate(names))
+                  + f" (stages {c[15]}, {c[15] / R:.1f} per row)", flush=True)
     os.environ["DPATHSIM_ABLATE"] = "8"
     timed(eng, R)
     c = eng.tensor("topk_ws")[:256].view(torch.int64).cpu().tolist()
