@@ -83,6 +83,25 @@ __device__ __forceinline__ int mneed_lo(double kth, int64_t den) {
   return static_cast<int>(ceil(r));
 }
 
+// The same threshold in fp32 (the per-stage thresholds and tile bounds are
+// pure filters: any value <= m* is sound, a smaller one only admits more
+// candidates to the exact fp64 score).  Inputs: kth as float, den as the sum of
+// two non-negative int64 converted by i64_f32 (relative error <= 3*2^-24 each).
+// Every rounding here is round-to-nearest, so the computed product is at most
+// r*(1 + 7*2^-24) with r = kth*den/2; the factor (1 - 2^-19) (exact in fp32)
+// brings it below r*(1 - 2^-53) <= m*, hence ceil() <= m* as before.
+__device__ __forceinline__ float i64_f32(int64_t v) {   // v >= 0
+  const uint64_t u = static_cast<uint64_t>(v);
+  return __uint2float_rn(static_cast<uint32_t>(u >> 32)) * 4294967296.0f +
+         __uint2float_rn(static_cast<uint32_t>(u));
+}
+__device__ __forceinline__ int mneed_lo32(float kth, float den) {
+  if (!(kth > 0.0f) || !(den > 0.0f)) return 0;
+  const float r = kth * den * (0.5f * (1.0f - 0x1p-19f));
+  if (r >= 2147483000.0f) return INT32_MAX;
+  return static_cast<int>(ceilf(r));
+}
+
 // Register-resident sorted top-k of one wave: rank r*64 + lane in slot r.
 template <int KPL>
 struct TopK {
@@ -599,13 +618,13 @@ __device__ __forceinline__ void epilogue_u8(const CctParams& p, uint32_t* acc, T
 // This lane's segment threshold for stage S: targets of segment `lane` need
 // M >= mseg to possibly reach the larger of tau_sh and the wave's k-th score.
 template <int KPL>
-__device__ __forceinline__ int stage_mseg(const TopK<KPL>& top, const Stage& S, int64_t gx,
+__device__ __forceinline__ int stage_mseg(const TopK<KPL>& top, const Stage& S, float gxf,
                                           double tau_sh) {
   double tau_w = tau_sh;
   if (top.full() && top.kth_s > tau_w) tau_w = top.kth_s;
   int mseg = 1;
   if (tau_w > 0.0) {
-    const int mn = mneed_lo(tau_w, gx + S.gq);
+    const int mn = mneed_lo32(static_cast<float>(tau_w), gxf + i64_f32(S.gq));
     mseg = mn > 1 ? mn : 1;
   }
   return mseg;
@@ -669,6 +688,7 @@ struct Window {
   int v, c;
   uint32_t vT;   // v * T: first bucket of venue v
   uint32_t lo, hi, mx;
+  int64_t gmn;   // tile_gmin[tw], loaded one tile ahead
 };
 
 // Advance to the next tile that may hold a top-k target (d <= 64 rows).  The
@@ -677,10 +697,13 @@ struct Window {
 // scatter and epilogue.
 template <int NW>
 __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d, int lane,
-                                           int64_t gx, double tau_sh, int seg_shift,
+                                           float gxf, double tau_sh, int seg_shift,
                                            bool no_scatter, Stage& S) {
+  const float tauf = static_cast<float>(tau_sh);
   while (w.tw < p.T) {
     const int64_t t = w.tw++;
+    const int64_t gmn = w.gmn;
+    if (t + 1 < p.T) w.gmn = p.tile_gmin[t + 1];
     const uint32_t lo = w.lo, hi = w.hi;
     // UB = sum_v C[x,v] * maxc[v,t] in 32 bits: a lane product of 2^25 or more
     // (or such a total) means "unbounded" -- no skip, 32-bit passes
@@ -694,7 +717,7 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
       w.mx = p.tile_maxc[vb];
     }
     if (!p.use_bounds) ub = int64_t(1) << 40;
-    const bool take = ub > 0 && (tau_sh <= 0.0 || ub >= mneed_lo(tau_sh, gx + p.tile_gmin[t]));
+    const bool take = ub > 0 && (tau_sh <= 0.0 || ub >= mneed_lo32(tauf, gxf + i64_f32(gmn)));
     if ((kProfile && (p.ablate & 8)) && threadIdx.x == 0) {   // counters: tiles visited, tiles scanned
       atomicAdd(p.counter + 4, 1ull);
       if (take) atomicAdd(p.counter + 5, 1ull);
@@ -755,6 +778,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
     const int d = static_cast<int>(p.c_ptr[x + 1] - pb);
     DPS_DASSERT(d >= 0);
     const int64_t gx = p.g[x];
+    const float gxf = i64_f32(gx);
     TopK<KPL> top;
     top.init(p.k);
     double tau_sh = -1.0;   // best k-th score of the workgroup, two stages old
@@ -769,6 +793,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       w.v = 0; w.c = 0;
       w.lo = w.hi = w.mx = 0;
       w.vT = 0;
+      w.gmn = p.tile_gmin[0];
       if (lane < d) {
         w.v = p.c_col[pb + lane];
         w.c = p.c_val[pb + lane];
@@ -779,7 +804,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         w.mx = p.tile_maxc[vb];
       }
       Stage cur;
-      bool have = find_stage<NW>(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, cur);
+      bool have = find_stage<NW>(p, w, d, lane, gxf, tau_sh, seg_shift, no_scatter, cur);
       // Batch 0 of the current stage is loaded one epilogue ahead.  It is issued
       // unconditionally (a missing stage loads dead chunks with C = 0) so B has
       // one definition in the loop and the register allocator need not copy it
@@ -820,13 +845,13 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
         for (int i = 1; i < NW; ++i) tm = tau_s[n & 1][i] > tm ? tau_s[n & 1][i] : tm;
         tau_sh = tm;
-        const int mseg = stage_mseg(top, cur, gx, tau_sh);
+        const int mseg = stage_mseg(top, cur, gxf, tau_sh);
         // find the next stage and put its first loads in flight before this
         // stage's epilogue (pure LDS work unless the queue fills up)
         Stage nxt;
         bool have_n;
         if (cur.pass + 1 < (1 << cur.lnp)) { nxt = cur; ++nxt.pass; have_n = true; }
-        else have_n = find_stage<NW>(p, w, d, lane, gx, tau_sh, seg_shift, no_scatter, nxt);
+        else have_n = find_stage<NW>(p, w, d, lane, gxf, tau_sh, seg_shift, no_scatter, nxt);
         if (!have_n) nxt.G.nq = 0;
         if (prof) ts[4] = __builtin_amdgcn_s_memtime();
         issue<NW>(nxt, 0, p.tile_ent, wave, lane, B, no_add, p.ablate, p.counter);
@@ -864,7 +889,8 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         ub = wave_sum(ub);
         if (!p.use_bounds) ub = int64_t(1) << 40;
         if (ub == 0) continue;
-        if (tau_sh > 0.0 && ub < mneed_lo(tau_sh, gx + p.tile_gmin[t])) continue;
+        if (tau_sh > 0.0 && ub < mneed_lo32(static_cast<float>(tau_sh), gxf + i64_f32(p.tile_gmin[t])))
+          continue;
         Stage S;
         S.t = t;
         S.lnp = ub <= 0xFF ? 0 : ub <= 0xFFFF ? 1 : 2;
@@ -901,7 +927,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
           for (int i = 1; i < NW; ++i) tm = tau_s[n & 1][i] > tm ? tau_s[n & 1][i] : tm;
           tau_sh = tm;
           epilogue<KPL, NW>(p, acc, top, Q, S, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh,
-                        stage_mseg(top, S, gx, tau_sh));
+                        stage_mseg(top, S, gxf, tau_sh));
           if (!p.dbuf) __syncthreads();
           ++n;
         }

@@ -626,11 +626,32 @@ __global__ __launch_bounds__(kBlock) void k_row_terms(const int64_t* __restrict_
                                                       int64_t n_rows,
                                                       const unsigned* __restrict__ n_v,
                                                       int64_t* __restrict__ terms) {
-  for (int64_t x = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; x < n_rows;
-       x += static_cast<int64_t>(gridDim.x) * kBlock) {
-    int64_t t = 0;
-    for (int64_t j = c_ptr[x]; j < c_ptr[x + 1]; ++j) t += n_v[c_col[j]];
-    terms[x] = t;
+  // as k_global_walks: a wave owns 64 consecutive rows and walks their entries
+  // in coalesced 64-entry strips, summing per row in LDS
+  __shared__ unsigned long long acc[kWavesPerBlock][kWave];
+  const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  for (int64_t r0 = wave0 * kWave; r0 < n_rows; r0 += nwaves * kWave) {
+    const int64_t x = r0 + lane;
+    const int64_t base = c_ptr[r0];
+    const int64_t xe = x < n_rows ? x : n_rows;
+    const uint32_t excl = static_cast<uint32_t>(c_ptr[xe] - base);
+    const uint32_t total = static_cast<uint32_t>(
+        c_ptr[r0 + kWave < n_rows ? r0 + kWave : n_rows] - base);
+    acc[wave][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t e0 = 0; e0 < total; e0 += kWave) {
+      const uint32_t i = e0 + lane;
+      const int o = wave_owner(excl, i);   // every lane takes part in the shuffles
+      if (i < total) atomicAdd(&acc[wave][o], static_cast<unsigned long long>(n_v[c_col[base + i]]));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (x < n_rows) terms[x] = static_cast<int64_t>(acc[wave][lane]);
+    __builtin_amdgcn_wave_barrier();
   }
 }
 

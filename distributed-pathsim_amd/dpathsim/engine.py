@@ -48,6 +48,8 @@ class Bounds:
     expand: int = 1      # >= sum_{x author} sum_{p in AP[x]} |PX[p]| (SpGEMM expansion)
     sum_c: int = 1       # >= sum of C over all AP rows (>= sum of s)
     key_bits: int = 1    # >= bit length of max g (and of max M[x,x])
+    max_row_expand: int = 1   # >= max over AP rows of sum_{p in AP[row]} |PX[p]|
+    max_mids_per_paper: int = 0   # >= max |PX[p]| (raw edges, before distinct)
 
 
 DENOMINATORS = ("rowsum", "diag")
@@ -166,18 +168,29 @@ class PathSimEngine:
             del ap_r, ap_c, px_r, px_c
             mark("csr")
             # A3: SpGEMM C = W_AP . W_PX over EVERY AP row (author rows [0, NA)
-            # first, then untyped author_of sources): capacities from the raw-edge
-            # bound (expand >= nnz C), no size read-back
-            expand = bnd.sum_c
-            sws = self._ws(_lib.size("dps_spgemm_workspace_size", N, expand))
+            # first, then untyped author_of sources), capacities from the
+            # raw-edge bounds (sum_c >= nnz C), no size read-back.  Papers with
+            # at most one mid (APVPA): gather + segmented unique; otherwise the
+            # hash SpGEMM.
+            cap = bnd.sum_c
             c_ptr, c_nnz = self._empty(N + 1, torch.int64), self._empty(2, torch.int64)
-            _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, N, _ptr(px_ptr),
-                      _ptr(px_col), NP, _ptr(c_ptr), None, None, _ptr(c_nnz), expand, _ptr(sws),
-                      sws.numel(), st)
-            c_col, c_val = self._empty(expand, torch.int32), self._empty(expand, torch.int32)
-            _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, N, _ptr(px_ptr),
-                      _ptr(px_col), NP, _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(c_nnz),
-                      expand, _ptr(sws), sws.numel(), st)
+            sp_status = self._empty(1, torch.int32)
+            c_col, c_val = self._empty(cap, torch.int32), self._empty(cap, torch.int32)
+            if bnd.max_mids_per_paper <= 1:
+                sws = self._ws(_lib.size("dps_spgemm_single_workspace_size", N, E, NP))
+                sp_status.zero_()
+                for numeric in (False, True):
+                    _lib.call("dps_spgemm_single", _ptr(ap_ptr), _ptr(ap_col), N, E, _ptr(px_ptr),
+                              _ptr(px_col), NP, _ptr(c_ptr), _ptr(c_col) if numeric else None,
+                              _ptr(c_val) if numeric else None, _ptr(c_nnz), _ptr(sws),
+                              sws.numel(), st)
+            else:
+                sws = self._ws(_lib.size("dps_spgemm_hash_workspace_size", N, bnd.max_row_expand))
+                for numeric in (False, True):
+                    _lib.call("dps_spgemm_hash", _ptr(ap_ptr), _ptr(ap_col), None, N, _ptr(px_ptr),
+                              _ptr(px_col), bnd.max_row_expand, _ptr(c_ptr),
+                              _ptr(c_col) if numeric else None, _ptr(c_val) if numeric else None,
+                              _ptr(c_nnz), _ptr(sp_status), _ptr(sws), sws.numel(), st)
             del sws
             mark("spgemm")
             # A4: s = column sums of C over ALL AP rows, g = C.s over author rows,
@@ -222,7 +235,7 @@ class PathSimEngine:
                  c_col=c_col, c_val=c_val, c_nnz=c_nnz, s=s, g=g, diag=diag, den=den, g_t=g_t,
                  t_perm=t_perm, t_rank=t_rank, tile_off=tile_off, tile_ent=tile_ent,
                  tile_maxc=tile_maxc, tile_gmin=tile_gmin, stats=stats, status=status,
-                 ap_nnz=ap_nnz, px_nnz=px_nnz,
+                 ap_nnz=ap_nnz, px_nnz=px_nnz, sp_status=sp_status,
                  topk_ws=self._ws(_lib.size("dps_cct_topk_workspace_size")))
         self.built = True
         if timed:
@@ -241,7 +254,7 @@ class PathSimEngine:
         d = self._dev
         info = self.info
         host = torch.cat([d["stats"], d["ap_nnz"], d["px_nnz"], d["c_nnz"][:1],
-                          d["status"].to(torch.int64)]).cpu()
+                          d["status"].to(torch.int64), d["sp_status"].to(torch.int64)]).cpu()
         # nnz over the author rows (C also holds the untyped author_of rows)
         L = _lib.STATS_LEN
         info.max_c = int(host[_lib.STAT_MAX_C])
@@ -252,6 +265,8 @@ class PathSimEngine:
         info.nnz_c = int(host[_lib.STAT_NNZ_C])
         info.expand = int(host[L + 2])         # nnz of C over every AP row
         status_h = int(host[L + 3])
+        if int(host[L + 4]) != 0:             # impossible by construction (raw >= distinct)
+            raise RuntimeError("a row's SpGEMM expansion exceeds its host bound")
         if info.expand > self.bounds.sum_c:   # impossible by construction (raw >= distinct)
             raise RuntimeError(f"nnz(C) {info.expand} exceeds its bound {self.bounds.sum_c}")
         if status_h != 0 or info.max_c > 0xFFFF:
@@ -406,7 +421,7 @@ def host_bounds(typed: TypedTables) -> Bounds:
     g = typed.graph
     NA, NP, NV = typed.n_authors, typed.n_papers, typed.n_mids
     if g.n_edges == 0 or NP == 0:
-        return Bounds()
+        return Bounds()   # (max_mids_per_paper 0: the single-mid SpGEMM)
     src, dst, rel = g.edge_src, g.edge_dst, typed.edge_rel
     nt = typed.node_type
     ap = (rel == L.R_AP) & (nt[dst] == L.T_PAPER)
@@ -426,7 +441,10 @@ def host_bounds(typed: TypedTables) -> Bounds:
     c_row_max = int(row_c.max()) if NA else 0
     # g[x] <= (sum_v C[x,v]) * max_v s_v;  M[x,x] <= (sum_v C[x,v])^2 <= that too
     gb = max(c_row_max * max(s_max, c_row_max), 1)
-    return Bounds(expand=max(expand, 1), sum_c=max(sum_c, 1), key_bits=min(64, gb.bit_length()))
+    row_all = np.bincount(ap_row, weights=per_edge, minlength=1)
+    return Bounds(expand=max(expand, 1), sum_c=max(sum_c, 1), key_bits=min(64, gb.bit_length()),
+                  max_row_expand=max(int(row_all.max()), 1),
+                  max_mids_per_paper=int(pxdeg.max()) if NP else 0)
 
 
 def build_engine(typed: TypedTables, device=None, tile_w=DEFAULT_TILE_W, timed=False,

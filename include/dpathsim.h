@@ -132,6 +132,38 @@ int dps_spgemm_count(const int64_t* ap_ptr, const int32_t* ap_col,
                      int64_t* c_ptr, int32_t* c_col, int32_t* c_val, int64_t* c_nnz,
                      int64_t expand_cap, void* ws, size_t ws_bytes, void* stream);
 
+/* A3, the engine's SpGEMM: wavefront-cooperative hash SpGEMM for the same C
+ * (output row i = AP row rows[i], or i when rows == NULL; columns ascending).
+ * No expanded intermediate array: per row, L = sum_{p in AP[row]} |PX[p]|
+ * picks a lane (L <= 16: register sorting network), a workgroup with an LDS
+ * hash table (L <= 4096) or a workgroup sorting in a global scratch region
+ * (L > 4096).  Two enqueue-only phases with one workspace:
+ *   symbolic (c_col == NULL): c_ptr int64[n_out_rows+1], *c_nnz (device);
+ *   numeric  (c_col != NULL): c_col/c_val int32[nnz] -- same, unmodified ws.
+ * max_row_expand >= max over rows of L (a host bound, e.g. from the raw
+ * edges); a row beyond it sets *status_dev = DPS_ERR_OVERFLOW (nullable). */
+size_t dps_spgemm_hash_workspace_size(int64_t n_out_rows, int64_t max_row_expand);
+int dps_spgemm_hash(const int64_t* ap_ptr, const int32_t* ap_col, const int32_t* rows,
+                    int64_t n_out_rows, const int64_t* px_ptr, const int32_t* px_col,
+                    int64_t max_row_expand, int64_t* c_ptr, int32_t* c_col, int32_t* c_val,
+                    int64_t* c_nnz, int32_t* status_dev, void* ws, size_t ws_bytes, void* stream);
+
+/* A3 when every paper has at most one mid (APVPA: one venue per paper): the
+ * expansion of row a IS its AP segment with each paper replaced by its mid,
+ * so C comes from one coalesced gather per AP entry plus a segmented sort +
+ * unique over the AP rows (a paper -> mid map of n_papers entries first makes
+ * that gather one random read).  Output rows = AP rows [0, n_out_rows) (ap_ptr with
+ * n_out_rows + 1 entries; the AP CSR must cover exactly these rows).
+ * nnz_ap_cap >= ap_ptr[n_out_rows] sizes the workspace.  Same two phases as
+ * dps_spgemm_hash.  A paper with two or more mids is a caller error (the
+ * engine chooses this path only when the raw edges give no paper two). */
+size_t dps_spgemm_single_workspace_size(int64_t n_out_rows, int64_t nnz_ap_cap,
+                                        int64_t n_papers);
+int dps_spgemm_single(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_out_rows,
+                      int64_t nnz_ap_cap, const int64_t* px_ptr, const int32_t* px_col,
+                      int64_t n_papers, int64_t* c_ptr, int32_t* c_col, int32_t* c_val,
+                      int64_t* c_nnz, void* ws, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------
  * A4. Global walk ingredients.
  * dps_mid_walks: s[v] = sum over ALL AP rows r of C[r,v]

@@ -151,3 +151,46 @@ def test_topk_rows_matches_contiguous_launch():
         assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
                               (b.view(np.int64) if b.dtype == np.float64 else b)[rows])
     assert all(a.shape[0] == 0 for a in eng.topk_rows(10, np.zeros(0, np.int64)))
+
+
+@pytest.mark.parametrize("multi", [1, 3])
+def test_spgemm_long_and_huge_rows(multi):
+    """The hash SpGEMM's three row paths: lane (L <= 16), LDS hash (16 < L <=
+    4096) and global-scratch sort (L > 4096), with papers of 1 or up to 3
+    venues each (repeats dropped by the PX distinct) -- C, g and the top-k
+    against the oracle."""
+    import pathsim_oracle as po
+    from dpathsim.engine import build_engine
+    from dpathsim.graph import Graph
+    rng = np.random.default_rng(multi)
+    papers_of = [5200, 1500, 40, 17, 3] + [1] * 2000
+    na, nv = len(papers_of), 400
+    n_pap = sum(papers_of)
+    src, dst = [], []
+    pid = 0
+    for a, n in enumerate(papers_of):
+        for _ in range(n):
+            src.append(a), dst.append(na + pid)
+            pid += 1
+    # a few shared papers between the heavy authors and the light ones
+    for _ in range(300):
+        src.append(int(rng.integers(0, na))), dst.append(na + int(rng.integers(0, 6000)))
+    n_ap = len(src)
+    for p in range(n_pap):
+        for _ in range(int(rng.integers(1, multi + 1))):
+            src.append(na + p), dst.append(na + n_pap + int(rng.integers(0, nv)))
+    types = np.concatenate([np.zeros(na), np.ones(n_pap), np.full(nv, 2)]).astype(np.int32)
+    rel = np.concatenate([np.zeros(n_ap), np.ones(len(src) - n_ap)]).astype(np.int32)
+    g = Graph(types, ["author", "paper", "venue"], np.array(src), np.array(dst), rel,
+              ["author_of", "submit_at"], node_ids=lambda i: f"n{i}", labels=lambda i: f"L{i}")
+    t = g.typed()
+    eng = build_engine(t, tile_w=1024)
+    co = po.COracle.from_typed(t)
+    cp, cc, cv, s, gg = co.export()
+    nnz = eng.info.nnz_c
+    assert np.array_equal(eng.tensor("c_ptr")[: na + 1].cpu().numpy(), cp)
+    assert np.array_equal(eng.tensor("c_col")[:nnz].cpu().numpy(), cc)
+    assert np.array_equal(eng.tensor("c_val")[:nnz].cpu().numpy(), cv)
+    assert np.array_equal(eng.tensor("s")[:nv].cpu().numpy(), s)
+    assert np.array_equal(eng.tensor("g")[:na].cpu().numpy(), gg)
+    _same([a.cpu().numpy() for a in eng.topk(10)], co.topk(10, 0, na))
