@@ -182,6 +182,15 @@ struct CctParams {
   int64_t row_begin;
   const int32_t* row_order;  // nullable: dequeue order of the rows (e.g. heaviest first)
   bool out_by_slot;          // output row = dequeue slot (dps_cct_topk_rows), else x - row_begin
+  // split rows: dequeue slots r < n_pieces are row PIECES -- target tiles
+  // [piece_t0[r], piece_t1[r]) of row row_order[r] -- whose ranked entries go
+  // to piece_*[r] with no zero-score fill (dps_topk_merge completes the rows)
+  int64_t n_pieces;
+  const int32_t* piece_t0;
+  const int32_t* piece_t1;
+  int32_t* piece_idx;
+  int64_t* piece_cnt;
+  double* piece_score;
   int64_t n_rows;
   int k;
   int32_t* out_idx;
@@ -685,6 +694,7 @@ __device__ __forceinline__ void epilogue(const CctParams& p, uint32_t* acc, TopK
 // (v_j, tw) is tile_ent[lo, hi), its largest C is mx.
 struct Window {
   int64_t tw;
+  int64_t tend;  // one past the last tile of this row (or row piece)
   int v, c;
   uint32_t vT;   // v * T: first bucket of venue v
   uint32_t lo, hi, mx;
@@ -700,10 +710,10 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
                                            float gxf, double tau_sh, int seg_shift,
                                            bool no_scatter, Stage& S) {
   const float tauf = static_cast<float>(tau_sh);
-  while (w.tw < p.T) {
+  while (w.tw < w.tend) {
     const int64_t t = w.tw++;
     const int64_t gmn = w.gmn;
-    if (t + 1 < p.T) w.gmn = p.tile_gmin[t + 1];
+    if (t + 1 < w.tend) w.gmn = p.tile_gmin[t + 1];
     const uint32_t lo = w.lo, hi = w.hi;
     // UB = sum_v C[x,v] * maxc[v,t] in 32 bits: a lane product of 2^25 or more
     // (or such a total) means "unbounded" -- no skip, 32-bit passes
@@ -711,7 +721,7 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
     const uint32_t ub32 = wave_sum_u32(prod > (1u << 25) ? (1u << 25) : static_cast<uint32_t>(prod));
     int64_t ub = ub32 >= (1u << 25) ? (int64_t(1) << 40) : static_cast<int64_t>(ub32);
     w.lo = hi;
-    if (lane < d && t + 1 < p.T) {
+    if (lane < d && t + 1 < w.tend) {
       const uint32_t vb = w.vT + static_cast<uint32_t>(t) + 1u;   // < V*T + 1 < 2^32
       w.hi = p.tile_off[vb + 1];
       w.mx = p.tile_maxc[vb];
@@ -771,8 +781,13 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
     const int64_t r = row_s;
     if (r >= p.n_rows) break;
     const int64_t x = p.row_order ? static_cast<int64_t>(p.row_order[r]) : p.row_begin + r;
-    const int64_t ro = p.out_by_slot ? r : x - p.row_begin;   // output row
-    DPS_DASSERT(ro >= 0 && ro < p.n_rows);
+    const bool is_piece = r < p.n_pieces;
+    const int64_t ro = (is_piece || p.out_by_slot) ? r : x - p.row_begin;   // output row
+    DPS_DASSERT(ro >= 0);
+    // target tiles of this slot: the whole row, or one piece of a split row
+    const int64_t t_beg = is_piece ? static_cast<int64_t>(p.piece_t0[r]) : 0;
+    const int64_t t_end = is_piece ? static_cast<int64_t>(p.piece_t1[r]) : p.T;
+    DPS_DASSERT(0 <= t_beg && t_beg <= t_end && t_end <= p.T);
     const int64_t x_lab = p.t_rank ? static_cast<int64_t>(p.t_rank[x]) : x;
     const int64_t pb = p.c_ptr[x];
     const int d = static_cast<int>(p.c_ptr[x + 1] - pb);
@@ -789,16 +804,17 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       // a wave that finished scanning stage n goes straight on to stage n+1's
       // loads and adds while the others still scan: one barrier per stage.
       Window w;
-      w.tw = 0;
+      w.tw = t_beg;
+      w.tend = t_end;
       w.v = 0; w.c = 0;
       w.lo = w.hi = w.mx = 0;
       w.vT = 0;
-      w.gmn = p.tile_gmin[0];
-      if (lane < d) {
+      w.gmn = t_beg < t_end ? p.tile_gmin[t_beg] : 0;
+      if (lane < d && t_beg < t_end) {
         w.v = p.c_col[pb + lane];
         w.c = p.c_val[pb + lane];
         w.vT = static_cast<uint32_t>(w.v) * static_cast<uint32_t>(p.T);
-        const int64_t vb = w.vT;
+        const int64_t vb = w.vT + static_cast<uint32_t>(t_beg);
         w.lo = p.tile_off[vb];
         w.hi = p.tile_off[vb + 1];
         w.mx = p.tile_maxc[vb];
@@ -878,7 +894,7 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       }
     } else if (d > kWave) {
       // ---- rows with more than 64 venues: the same stages, synchronously
-      for (int64_t t = 0; t < p.T; ++t) {
+      for (int64_t t = t_beg; t < t_end; ++t) {
         int64_t ub = 0;
         for (int g0 = 0; g0 < d; g0 += kWave) {
           const int j = g0 + lane;
@@ -964,16 +980,16 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         }
       }
       // ranked entries, then zero-score targets in reference order, then -1
-      int32_t* oi = p.out_idx + ro * p.k;
-      int64_t* oc = p.out_cnt + ro * p.k;
-      double* os = p.out_score + ro * p.k;
+      int32_t* oi = (is_piece ? p.piece_idx : p.out_idx) + ro * p.k;
+      int64_t* oc = (is_piece ? p.piece_cnt : p.out_cnt) + ro * p.k;
+      double* os = (is_piece ? p.piece_score : p.out_score) + ro * p.k;
 #pragma unroll
       for (int q = 0; q < KPL; ++q) {
         const int slot = q * kWave + lane;
         if (slot < top.filled) { oi[slot] = top.y[q]; oc[slot] = top.m[q]; os[slot] = top.s[q]; }
       }
       const int64_t avail = p.n_targets - 1;
-      const int want = static_cast<int>(avail < p.k ? avail : p.k);
+      const int want = is_piece ? top.filled : static_cast<int>(avail < p.k ? avail : p.k);
       int slot = top.filled;
       for (int64_t yb = 0; slot < want && yb < p.n_targets; yb += kWave) {
         const int64_t yc = yb + lane;
@@ -1003,6 +1019,87 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       __syncthreads();
       for (int i = tid; i < NW * p.k * 4; i += NW * kWave) lds[i] = 0;   // 16 B per merge entry
     }
+  }
+}
+
+// Split rows: one wave per row merges the ranked lists of its P pieces (each
+// sorted by (score desc, y asc), -1 after its last entry) -- lane j holds the
+// head of list j, a wave arg-best picks the next entry -- then fills zero-score
+// targets in reference order and -1, exactly as the kernel's row end does.
+constexpr int kMergeMaxK = 256;
+
+__global__ __launch_bounds__(256) void k_topk_merge(
+    const int32_t* __restrict__ p_idx, const int64_t* __restrict__ p_cnt,
+    const double* __restrict__ p_score, const int32_t* __restrict__ rows, int64_t n_groups, int P,
+    int k, int64_t n_targets, int64_t row_begin, int32_t* __restrict__ out_idx,
+    int64_t* __restrict__ out_cnt, double* __restrict__ out_score) {
+  __shared__ int32_t ranked_s[4][kMergeMaxK];
+  const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
+  int32_t* ranked = ranked_s[wave];
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * (blockDim.x / kWave);
+  for (int64_t grp = wave0; grp < n_groups; grp += nwaves) {
+    const int64_t x = rows[grp * P];
+    const int64_t ro = x - row_begin;
+    int32_t* oi = out_idx + ro * k;
+    int64_t* oc = out_cnt + ro * k;
+    double* os = out_score + ro * k;
+    const int64_t base = (grp * P + lane) * static_cast<int64_t>(k);   // list of lane j
+    int h = 0;
+    double hs = -1.0;
+    int hy = INT_MAX;
+    if (lane < P && p_idx[base] >= 0) { hs = p_score[base]; hy = p_idx[base]; }
+    int filled = 0;
+    for (; filled < k; ++filled) {
+      // wave arg-best over the heads (score desc, then y asc)
+      double bs = hs;
+      int by = hy, bl = lane;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const double os2 = __shfl_xor(bs, off, kWave);
+        const int oy = __shfl_xor(by, off, kWave);
+        const int ol = __shfl_xor(bl, off, kWave);
+        if (better(os2, oy, bs, by)) { bs = os2; by = oy; bl = ol; }
+      }
+      if (by == INT_MAX) break;   // every list is exhausted
+      if (lane == bl) {
+        const int64_t e = base + h;
+        oi[filled] = hy;
+        oc[filled] = p_cnt[e];
+        os[filled] = hs;
+        ranked[filled] = hy;
+        ++h;
+        hs = -1.0;
+        hy = INT_MAX;
+        if (h < k && p_idx[base + h] >= 0) { hs = p_score[base + h]; hy = p_idx[base + h]; }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t avail = n_targets - 1;
+    const int want = static_cast<int>(avail < k ? avail : k);
+    int slot = filled;
+    for (int64_t yb = 0; slot < want && yb < n_targets; yb += kWave) {
+      const int64_t yc = yb + lane;
+      bool ok = yc < n_targets && yc != x;
+      for (int q = 0; q < filled && ok; ++q) ok = ranked[q] != static_cast<int>(yc);
+      const uint64_t mk = ballot(ok);
+      const int rank = mbcnt(mk);
+      if (ok && slot + rank < want) {
+        oi[slot + rank] = static_cast<int32_t>(yc);
+        oc[slot + rank] = 0;
+        os[slot + rank] = 0.0;
+      }
+      slot += __popcll(mk);
+    }
+    for (int s2 = want + lane; s2 < k; s2 += kWave) {
+      oi[s2] = -1;
+      oc[s2] = 0;
+      os[s2] = 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1073,7 +1170,10 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
                          const uint32_t* tile_maxc, const int64_t* tile_gmin, int64_t row_begin,
                          int64_t n_rows, const int32_t* row_order, bool out_by_slot, int32_t k,
                          int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
-                         size_t ws_bytes, void* stream) {
+                         size_t ws_bytes, void* stream, int64_t n_pieces = 0,
+                         const int32_t* piece_t0 = nullptr, const int32_t* piece_t1 = nullptr,
+                         int32_t* piece_idx = nullptr, int64_t* piece_cnt = nullptr,
+                         double* piece_score = nullptr) {
   const int shift = log2_exact(tile_w);
   DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED,
               "tile_w must be a power of two in [256, 65536], got %d", tile_w);
@@ -1107,6 +1207,8 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
 
   p.dbuf = nw > 1 && shift <= 14;   // 2 x W bytes of u8 accumulators up to W = 16384, one 32 KB buffer above
   p.row_begin = row_begin; p.row_order = row_order; p.out_by_slot = out_by_slot;
+  p.n_pieces = n_pieces; p.piece_t0 = piece_t0; p.piece_t1 = piece_t1;
+  p.piece_idx = piece_idx; p.piece_cnt = piece_cnt; p.piece_score = piece_score;
   p.n_rows = n_rows; p.k = k;
   p.out_idx = out_idx; p.out_cnt = out_cnt; p.out_score = out_score;
   p.counter = static_cast<unsigned long long*>(ws);
@@ -1149,6 +1251,50 @@ int dps_cct_topk_rows(const int64_t* c_ptr, const int32_t* c_col, const int32_t*
   return cct_topk_impl(c_ptr, c_col, c_val, g, g_t, t_perm, t_rank, n_targets, n_mids, tile_w,
                        tile_off, tile_ent, tile_maxc, tile_gmin, 0, n_rows, rows, true, k,
                        out_idx, out_cnt, out_score, ws, ws_bytes, stream);
+}
+
+int dps_cct_topk_split(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                       const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
+                       const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                       const uint32_t* tile_off, const uint32_t* tile_ent,
+                       const uint32_t* tile_maxc, const int64_t* tile_gmin, int64_t row_begin,
+                       int64_t row_end, const int32_t* row_order, int64_t n_order,
+                       const int32_t* piece_t0, const int32_t* piece_t1, int64_t n_pieces,
+                       int32_t* piece_idx, int64_t* piece_cnt, double* piece_score, int32_t k,
+                       int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
+                       size_t ws_bytes, void* stream) {
+  DPS_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= n_targets, DPS_ERR_INVALID,
+              "row range [%lld, %lld) outside [0, %lld)", static_cast<long long>(row_begin),
+              static_cast<long long>(row_end), static_cast<long long>(n_targets));
+  DPS_REQUIRE(n_pieces >= 0 && n_order >= n_pieces, DPS_ERR_INVALID, "bad n_order / n_pieces");
+  DPS_REQUIRE(n_order - n_pieces <= row_end - row_begin, DPS_ERR_INVALID,
+              "more whole rows than the range holds");
+  DPS_REQUIRE(n_order == 0 || row_order, DPS_ERR_INVALID, "row_order is required");
+  DPS_REQUIRE(n_pieces == 0 || (piece_t0 && piece_t1 && piece_idx && piece_cnt && piece_score),
+              DPS_ERR_INVALID, "piece ranges and outputs are required");
+  return cct_topk_impl(c_ptr, c_col, c_val, g, g_t, t_perm, t_rank, n_targets, n_mids, tile_w,
+                       tile_off, tile_ent, tile_maxc, tile_gmin, row_begin, n_order, row_order,
+                       false, k, out_idx, out_cnt, out_score, ws, ws_bytes, stream, n_pieces,
+                       piece_t0, piece_t1, piece_idx, piece_cnt, piece_score);
+}
+
+int dps_topk_merge(const int32_t* piece_idx, const int64_t* piece_cnt, const double* piece_score,
+                   const int32_t* rows, int64_t n_groups, int32_t pieces_per_row, int32_t k,
+                   int64_t n_targets, int64_t row_begin, int32_t* out_idx, int64_t* out_cnt,
+                   double* out_score, void* stream) {
+  DPS_REQUIRE(n_groups >= 0 && pieces_per_row >= 1 && pieces_per_row <= kWave, DPS_ERR_INVALID,
+              "pieces_per_row must be in [1, 64]");
+  DPS_REQUIRE(k >= 1 && k <= kMergeMaxK, DPS_ERR_UNSUPPORTED, "k must be in [1, 256]");
+  if (n_groups == 0) return DPS_OK;
+  DPS_REQUIRE(piece_idx && piece_cnt && piece_score && rows && out_idx && out_cnt && out_score,
+              DPS_ERR_INVALID, "null array");
+  auto st = static_cast<hipStream_t>(stream);
+  const unsigned grid = static_cast<unsigned>((n_groups + 3) / 4 < 2048 ? (n_groups + 3) / 4 : 2048);
+  k_topk_merge<<<grid, 256, 0, st>>>(piece_idx, piece_cnt, piece_score, rows, n_groups,
+                                     pieces_per_row, k, n_targets, row_begin, out_idx, out_cnt,
+                                     out_score);
+  DPS_LAUNCHED();
+  return DPS_OK;
 }
 
 }  // extern "C"

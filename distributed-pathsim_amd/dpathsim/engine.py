@@ -17,6 +17,8 @@ from . import _lib
 from .graph import TypedTables
 
 DEFAULT_TILE_W = 8192
+DEFAULT_SPLIT_ROWS = 256    # heaviest rows of a launch cut into pieces
+DEFAULT_PIECES = 16         # target-tile ranges per split row
 
 
 def _ptr(t):
@@ -79,6 +81,10 @@ class PathSimEngine:
         self.tile_w = int(tile_w)
         self.denominator = denominator
         self.tile_skip = True
+        # load balance of the hot kernel: the split_rows heaviest rows of a
+        # launch are cut into `pieces` target-tile ranges (see topk())
+        self.split_rows = DEFAULT_SPLIT_ROWS
+        self.pieces = DEFAULT_PIECES
         self.info = BuildInfo()
         self.bounds = None
         self.built = False
@@ -307,11 +313,16 @@ class PathSimEngine:
 
     # ------------------------------------------------------------------ top-k
     def topk(self, k: int, row_begin: int = 0, row_end: int | None = None, out=None,
-             heavy_first: bool = True):
+             heavy_first: bool = True, split_rows: int | None = None, pieces: int | None = None):
         """★ all-pairs top-k for author rows [row_begin, row_end) (device tensors).
 
         ``heavy_first`` dequeues the rows in descending ``row_work`` order (LPT),
-        so the few very heavy rows do not trail at the end of the launch; the
+        so the few very heavy rows do not trail at the end of the launch.  One
+        wave owns one row, so the ``split_rows`` heaviest rows of the range are
+        further cut into ``pieces`` target-tile ranges each (processed first, in
+        the same launch, by separate waves) and their piece lists merged after
+        (dps_topk_merge): a single heavy row then no longer bounds the launch --
+        which matters most for the small per-rank shards of an N-GPU run.  The
         results are identical either way."""
         if not self.built:
             raise RuntimeError("call build() first")
@@ -328,18 +339,41 @@ class PathSimEngine:
         idx, cnt, sc = out
         if R == 0:
             return idx, cnt, sc
+        T = max(1, math.ceil(NA / self.tile_w))
+        M = self.split_rows if split_rows is None else int(split_rows)
+        P = min(self.pieces if pieces is None else int(pieces), T, 64)
+        if not heavy_first or P < 2 or R <= 4 * M:
+            M = 0
+        common = (_ptr(d["c_ptr"]), _ptr(d["c_col"]), _ptr(d["c_val"]), _ptr(d["den"]),
+                  _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA, self.typed.n_mids,
+                  self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
+                  _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]))
         with torch.cuda.device(self.device):
             order = None
             if heavy_first and R > 1:
                 w = self.row_work()[row_begin:row_end]
                 order = (torch.argsort(w, descending=True, stable=True) + row_begin).to(torch.int32)
-            _lib.call("dps_cct_topk", _ptr(d["c_ptr"]), _ptr(d["c_col"]), _ptr(d["c_val"]),
-                      _ptr(d["den"]), _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA,
-                      self.typed.n_mids, self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
-                      _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]),
-                      int(row_begin), int(row_end), _ptr(order), int(k),
-                      _ptr(idx), _ptr(cnt), _ptr(sc), _ptr(d["topk_ws"]), d["topk_ws"].numel(),
-                      self.stream)
+            if M == 0:
+                _lib.call("dps_cct_topk", *common, int(row_begin), int(row_end), _ptr(order),
+                          int(k), _ptr(idx), _ptr(cnt), _ptr(sc), _ptr(d["topk_ws"]),
+                          d["topk_ws"].numel(), self.stream)
+                return idx, cnt, sc
+            # M heaviest rows -> M*P pieces first in the dequeue list, then the rest
+            heavy = order[:M]
+            part = torch.arange(P + 1, device=self.device, dtype=torch.int64) * T // P
+            t0 = part[:-1].to(torch.int32).repeat(M)
+            t1 = part[1:].to(torch.int32).repeat(M)
+            dq = torch.cat([heavy.repeat_interleave(P), order[M:]])
+            n_p = M * P
+            pbuf = (torch.empty((n_p, k), dtype=torch.int32, device=self.device),
+                    torch.empty((n_p, k), dtype=torch.int64, device=self.device),
+                    torch.empty((n_p, k), dtype=torch.float64, device=self.device))
+            _lib.call("dps_cct_topk_split", *common, int(row_begin), int(row_end), _ptr(dq),
+                      int(dq.numel()), _ptr(t0), _ptr(t1), n_p, _ptr(pbuf[0]), _ptr(pbuf[1]),
+                      _ptr(pbuf[2]), int(k), _ptr(idx), _ptr(cnt), _ptr(sc), _ptr(d["topk_ws"]),
+                      d["topk_ws"].numel(), self.stream)
+            _lib.call("dps_topk_merge", _ptr(pbuf[0]), _ptr(pbuf[1]), _ptr(pbuf[2]), _ptr(dq), M,
+                      P, int(k), NA, int(row_begin), _ptr(idx), _ptr(cnt), _ptr(sc), self.stream)
         return idx, cnt, sc
 
     def topk_rows(self, k: int, rows, out=None):

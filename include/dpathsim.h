@@ -284,6 +284,38 @@ int dps_cct_topk_rows(const int64_t* c_ptr, const int32_t* c_col, const int32_t*
                       int64_t n_rows, int32_t k, int32_t* out_idx, int64_t* out_cnt,
                       double* out_score, void* ws, size_t ws_bytes, void* stream);
 
+/* Load balance for the hot kernel (one wave owns one row, so a single very
+ * heavy row would bound a launch's time -- the N-GPU shards in particular):
+ *
+ * dps_cct_topk_split: one launch over [row_begin, row_end) whose dequeue list
+ *   row_order[0 .. n_order) starts with n_pieces row PIECES -- slot i <
+ *   n_pieces is source row row_order[i] restricted to the target tiles
+ *   [piece_t0[i], piece_t1[i]) (tile = tile_w consecutive target labels, T =
+ *   ceil(n_targets/tile_w)); its ranked targets (score > 0, order score desc
+ *   then y asc, -1 after them, no zero-score fill) go to row i of piece_* --
+ *   followed by whole rows, written to output row x - row_begin of out_* as
+ *   dps_cct_topk writes them.  Rows of the range listed neither way are left
+ *   untouched.  The pieces of one row must cover [0, T) exactly once.
+ * dps_topk_merge: for every group m of pieces_per_row consecutive piece slots
+ *   (all of one row x = rows[m * pieces_per_row]), merges their lists into the
+ *   row's exact top-k (the top-k of a union is the top-k of the members'
+ *   top-ks), adds the zero-score fill in reference order and -1, and writes
+ *   output row x - row_begin of out_*.  1 <= pieces_per_row <= 64. */
+int dps_cct_topk_split(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                       const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
+                       const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                       const uint32_t* tile_off, const uint32_t* tile_ent,
+                       const uint32_t* tile_maxc, const int64_t* tile_gmin, int64_t row_begin,
+                       int64_t row_end, const int32_t* row_order, int64_t n_order,
+                       const int32_t* piece_t0, const int32_t* piece_t1, int64_t n_pieces,
+                       int32_t* piece_idx, int64_t* piece_cnt, double* piece_score, int32_t k,
+                       int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
+                       size_t ws_bytes, void* stream);
+int dps_topk_merge(const int32_t* piece_idx, const int64_t* piece_cnt, const double* piece_score,
+                   const int32_t* rows, int64_t n_groups, int32_t pieces_per_row, int32_t k,
+                   int64_t n_targets, int64_t row_begin, int32_t* out_idx, int64_t* out_cnt,
+                   double* out_score, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Single-source row (the reference's run() loop, :30-50): for one sparse C row
  * (src_col/src_val, src_len entries, device), the dense pairwise walk

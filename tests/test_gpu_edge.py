@@ -194,3 +194,20 @@ def test_spgemm_long_and_huge_rows(multi):
     assert np.array_equal(eng.tensor("s")[:nv].cpu().numpy(), s)
     assert np.array_equal(eng.tensor("g")[:na].cpu().numpy(), gg)
     _same([a.cpu().numpy() for a in eng.topk(10)], co.topk(10, 0, na))
+
+
+@pytest.mark.parametrize("M,P,k", [(40, 4, 10), (300, 16, 10), (64, 7, 100), (5, 64, 3)])
+def test_split_rows_identical(M, P, k):
+    """Heavy rows cut into target-tile pieces (dps_cct_topk_split + the merge)
+    give exactly the unsplit rows, including the zero-score fill of rows with
+    fewer than k positive scores and row sub-ranges."""
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_dblp
+    t = synth_dblp(6000, 18000, 300, seed=13).typed()
+    eng = build_engine(t, tile_w=256)
+    whole = [a.cpu().numpy() for a in eng.topk(k, split_rows=0)]
+    for r0, r1 in ((0, 6000), (100, 2500)):
+        got = [a.cpu().numpy() for a in eng.topk(k, r0, r1, split_rows=M, pieces=P)]
+        for a, b in zip(got, whole):
+            assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
+                                  (b.view(np.int64) if b.dtype == np.float64 else b)[r0:r1])
