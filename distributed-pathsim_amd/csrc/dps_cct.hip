@@ -727,7 +727,9 @@ __device__ __forceinline__ bool find_stage(const CctParams& p, Window& w, int d,
       w.mx = p.tile_maxc[vb];
     }
     if (!p.use_bounds) ub = int64_t(1) << 40;
-    const bool take = ub > 0 && (tau_sh <= 0.0 || ub >= mneed_lo32(tauf, gxf + i64_f32(gmn)));
+    const bool take = (kProfile && (p.ablate & 64))   // profiling aid: no bound test
+                          ? true
+                          : ub > 0 && (tau_sh <= 0.0 || ub >= mneed_lo32(tauf, gxf + i64_f32(gmn)));
     if ((kProfile && (p.ablate & 8)) && threadIdx.x == 0) {   // counters: tiles visited, tiles scanned
       atomicAdd(p.counter + 4, 1ull);
       if (take) atomicAdd(p.counter + 5, 1ull);
@@ -872,7 +874,13 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
         if (prof) ts[4] = __builtin_amdgcn_s_memtime();
         issue<NW>(nxt, 0, p.tile_ent, wave, lane, B, no_add, p.ablate, p.counter);
         if (prof) ts[5] = __builtin_amdgcn_s_memtime();
-        epilogue<KPL, NW>(p, acc, top, Q, cur, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh, mseg);
+        if (kProfile && (p.ablate & 32)) {   // profiling aid: zero the accumulator only
+          for (int i = wave * (nbuf / NW) + lane * 4; i < (wave + 1) * (nbuf / NW); i += kWave * 4)
+            *reinterpret_cast<uint4*>(acc + i) = make_uint4(0, 0, 0, 0);
+        } else {
+          epilogue<KPL, NW>(p, acc, top, Q, cur, wave, lane, nbuf, seg_shift, x_lab, gx, tau_sh,
+                            mseg);
+        }
         if (prof) ts[6] = __builtin_amdgcn_s_memtime();
 #ifdef DPS_NOBAR2
         if constexpr (NW > 1)

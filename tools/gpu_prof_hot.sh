@@ -8,11 +8,11 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 export DPATHSIM_LIB=$PWD/distributed-pathsim_amd/dpathsim/libdpathsim_prof.so
-AB_W=8192 AB_ABLATE="1,2,4,16" timeout -k 10 300 python3 -u tools/ab_hot.py > gpurun_out/ab_hot.log 2>&1 \
+AB_W=8192 AB_ABLATE="${ABL_T:-1,2,4,32,64,16}" timeout -k 10 300 python3 -u tools/ab_hot.py > gpurun_out/ab_hot.log 2>&1 \
   || { echo "ab_hot failed"; tail -20 gpurun_out/ab_hot.log; exit 1; }
 cat gpurun_out/ab_hot.log
 P="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
-for a in 0 1 2 4; do
+for a in ${ABL_P:-0 1 2 4 32 64}; do
   rm -rf gpurun_out/valu_$a
   DPATHSIM_ABLATE=$a HOT_ROWS=200000 timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d gpurun_out/valu_$a -o run -- python3 -u tools/hot_once.py \
     > gpurun_out/valu_$a.log 2>&1 || { echo "pass $a failed"; tail -20 gpurun_out/valu_$a.log; exit 1; }
