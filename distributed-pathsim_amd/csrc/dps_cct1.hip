@@ -1,0 +1,417 @@
+// ★ Hot path, lean variant: the fused C.C^T + fp64 score + top-k kernel for the
+// bench shape -- tiles of W = 8192 targets with 16-bit entries, one wave per
+// source row, any row degree, k <= 256 (replaces
+// metapath_pairwise_walk DPathSim_APVPA.py:90-109, the score :51-52 and the
+// target loop :18-22,36).  Same operands, same results (bit for bit) as
+// k_cct_topk in dps_cct.hip; what differs is how the per-tile work is driven:
+//
+//   tile walk   the row's tile bounds UB[t] = sum_v C[x,v] * maxc[v,t] are
+//               computed 64 tiles at a time, lane = tile (coalesced maxc
+//               reads, no per-tile wave reduction), together with each tile's
+//               smallest g.  A 64-bit mask of the tiles that can still hold a
+//               top-k target is refiltered with one ballot whenever the row's
+//               k-th score tau rises; the next tile is the mask's lowest bit
+//               (scalar), so skipped tiles cost nothing and no load sits on
+//               the path from one tile to the next.
+//   pipeline    the next tile's bucket bounds are loaded one stage ahead and
+//               its first chunk batch is issued before this stage's epilogue,
+//               as in k_cct_topk; no barrier, no LDS round trip for tau.
+//   epilogue    the exact byte compare uses the single-form SWAR test when the
+//               segment threshold m <= 128 (every case that matters); the
+//               self-exclusion runs only in the source's own tile.
+//
+// Skipping a tile is sound for the same reason as in k_cct_topk: UB bounds
+// every M of the tile and mneed_lo32(tau, gx + gmin_t) is at most the
+// smallest M whose score can reach tau (ties included).
+#include "dps_cct_dev.hpp"
+
+#include <cstdlib>
+
+namespace dps {
+namespace {
+
+constexpr int kS1 = 13;                       // log2 W
+constexpr int kW1 = 1 << kS1;                 // 8192 targets per tile
+constexpr int kAcc1 = kW1 / 4;                // accumulator dwords (packed u8)
+constexpr int kSeg1 = 10;                     // threshold segments of 1024 targets
+constexpr uint32_t kLabMask1 = (kW1 - 1) & ~3u;
+
+// 64 consecutive tiles of one row: lane l describes tile w0 + l.
+struct Win1 {
+  int w0;          // first tile of the window (wave-uniform)
+  uint32_t ub;     // lane: UB of the tile (0xFFFFFFFF = unbounded)
+  float gmf;       // lane: smallest g of the tile, as float
+  uint64_t live;   // tiles not yet visited that may hold a top-k target
+  double tau;      // tau the mask was last filtered with
+};
+
+// UB of tiles w0 + lane over all d venues of the row (lane j of c / vT holds
+// venue j of the first 64; rows with more venues reload them per group).
+__device__ __forceinline__ uint32_t win_ub(const CctParams& p, int w0, int t_end, int64_t pb, int d,
+                                           int c, uint32_t vT, int lane) {
+  const int t = w0 + lane;
+  const bool in = t < t_end;
+  if (!p.use_bounds) return 0xFFFFFFFFu;        // no tile bounds: every tile, 32-bit passes
+  uint64_t acc = 0;
+  for (int g0 = 0; g0 < d; g0 += kWave) {
+    int cg = c;
+    uint32_t vg = vT;
+    if (g0 > 0) {
+      const int j = g0 + lane;
+      cg = j < d ? p.c_val[pb + j] : 0;
+      vg = j < d ? static_cast<uint32_t>(p.c_col[pb + j]) * static_cast<uint32_t>(p.T) : 0u;
+    }
+    const int nj = d - g0 < kWave ? d - g0 : kWave;
+#pragma unroll 4
+    for (int j = 0; j < nj; ++j) {
+      const uint32_t cj = readlane(static_cast<unsigned>(cg), j);
+      const uint32_t vj = readlane(vg, j);
+      const uint32_t mx = in ? p.tile_maxc[vj + static_cast<uint32_t>(t)] : 0u;
+      acc += static_cast<uint64_t>(cj) * mx;
+    }
+  }
+  return acc >= 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(acc);
+}
+
+// Tiles of the window whose bound reaches mneed(tau) (all of them while tau <= 0).
+__device__ __forceinline__ uint64_t win_pass(const Win1& w, double tau, float gxf) {
+  if (!(tau > 0.0)) return ~0ull;
+  const int mn = mneed_lo32(static_cast<float>(tau), gxf + w.gmf);
+  return ballot(w.ub >= static_cast<uint32_t>(mn));
+}
+
+__device__ __forceinline__ void win_load(const CctParams& p, Win1& w, int w0, int t_lo, int t_end,
+                                         int64_t pb, int d, int c, uint32_t vT, int lane,
+                                         double tau, float gxf) {
+  w.w0 = w0;
+  const int t = w0 + lane;
+  w.gmf = t < t_end ? i64_f32(p.tile_gmin[t]) : 0.0f;
+  w.ub = win_ub(p, w0, t_end, pb, d, c, vT, lane);
+  w.live = ballot(t >= t_lo && t < t_end && w.ub > 0) & win_pass(w, tau, gxf);
+  w.tau = tau;
+}
+
+// Next tile to process (-1: none left); slides the window as needed.
+__device__ __forceinline__ int next_tile(const CctParams& p, Win1& w, int t_end, int64_t pb, int d,
+                                         int c, uint32_t vT, int lane, double tau, float gxf,
+                                         uint32_t& ub_t) {
+  for (;;) {
+    if (w.live) {
+      const int b = __builtin_ctzll(w.live);
+      w.live &= w.live - 1;
+      ub_t = readlane(w.ub, b);
+      return w.w0 + b;
+    }
+    if (w.w0 + kWave >= t_end) return -1;
+    win_load(p, w, w.w0 + kWave, w.w0 + kWave, t_end, pb, d, c, vT, lane, tau, gxf);
+  }
+}
+
+// Bucket bounds of one tile (lane j < 64: venue j) and the smallest g of each of
+// its 8 threshold segments (lane s < 8), loaded one stage ahead.
+struct Pend1 {
+  int t;
+  uint32_t ub;
+  uint32_t lo, hi;
+  int64_t gs;
+};
+
+__device__ __forceinline__ void pend_load(const CctParams& p, Pend1& P, int t, uint32_t ub, int d0,
+                                          uint32_t vT, int lane) {
+  P.t = t;
+  P.ub = ub;
+  P.lo = P.hi = 0;
+  P.gs = 0;
+  if (t < 0) return;
+  if (lane < d0) {
+    P.lo = p.tile_off[vT + static_cast<uint32_t>(t)];
+    P.hi = p.tile_off[vT + static_cast<uint32_t>(t) + 1u];
+  }
+  if (lane < (kW1 >> kSeg1)) {
+    const int64_t i = (static_cast<int64_t>(t) << kS1) + (static_cast<int64_t>(lane) << kSeg1);
+    P.gs = p.g_t[i < p.n_targets ? i : p.n_targets - 1];
+  }
+}
+
+struct Stage1 {
+  Stage S;       // chunk group, tile, pass mode (shared helpers' view)
+  float gsf;     // lane s < 8: smallest g of segment s, as float
+};
+
+__device__ __forceinline__ void stage_make(Stage1& X, const Pend1& P, int c, int d0) {
+  X.S.t = P.t;
+  X.S.lnp = P.ub <= 0xFFu ? 0 : P.ub <= 0xFFFFu ? 1 : 2;
+  X.S.pass = 0;
+  grp_set(X.S.G, P.lo, P.hi, c, d0);
+  X.S.nb = (X.S.G.nq + kWave * kU - 1) / (kWave * kU);
+  X.S.gq = 0;
+  X.gsf = i64_f32(P.gs);
+}
+
+// Per-byte flags (bit 7) of a packed u8 dword: byte >= m, for 1 <= m <= 128.
+__device__ __forceinline__ uint32_t ge_u8_lo(uint32_t a, uint32_t kA) {
+  return (a | ((a & 0x7F7F7F7Fu) + kA)) & 0x80808080u;
+}
+
+// u8 epilogue over the whole tile: 8 blocks of 1024 targets (one threshold
+// segment each, lane l reads dwords 4l..4l+3 of the block), read and zeroed 4
+// at a time; candidates are queued and scored 64 at a time by flush().
+template <int KPL>
+__device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top, CandQ& Q,
+                                        int t, int lane, int64_t x_lab, int64_t gx, int mseg) {
+  const int64_t tile_base = static_cast<int64_t>(t) << kS1;
+  const int64_t xr = x_lab - tile_base;
+  const bool xin = xr >= 0 && xr < kW1;          // the source is a target of this tile
+  const int xrel = xin ? static_cast<int>(xr) : 0;
+  auto block = [&](uint4 a, int blk) {
+    const uint32_t m = static_cast<uint32_t>(readlane(mseg, blk));
+    if (m > 255u) return;                         // no u8 count reaches m
+    const uint32_t pm = (0x100u - (0x80000000u >> __builtin_clz(m))) * 0x01010101u;
+    if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) return;
+    uint32_t F;
+    if (m <= 128u) {
+      const uint32_t kA = (128u - m) * 0x01010101u;
+      F = ge_u8_lo(a.x, kA) | (ge_u8_lo(a.y, kA) >> 1) | (ge_u8_lo(a.z, kA) >> 2) |
+          (ge_u8_lo(a.w, kA) >> 3);
+    } else {
+      const uint32_t kA = (128u - m) * 0x01010101u, kB = (256u - m) * 0x01010101u;
+      F = ge_u8(a.x, kA, kB, false) | (ge_u8(a.y, kA, kB, false) >> 1) |
+          (ge_u8(a.z, kA, kB, false) >> 2) | (ge_u8(a.w, kA, kB, false) >> 3);
+    }
+    // target (4*dw + byte) of this lane's 16 -> bit 8*byte + 7 - dw
+    const int i0 = (blk << kSeg1) + (lane << 4);
+    if (xin) {                                    // the source itself never counts
+      const int rel = xrel - i0;
+      if (rel >= 0 && rel < 16) F &= ~(1u << ((rel & 3) * 8 + 7 - (rel >> 2)));
+    }
+    if (!ballot(F != 0)) return;
+    wave_lds_fence();
+    for (;;) {
+      const bool has = F != 0;
+      const uint64_t mk = ballot(has);
+      if (!mk) break;
+      if (has) {
+        const int bit = __builtin_ctz(F);
+        F &= F - 1;
+        const int byte = bit >> 3, dw = 7 - (bit & 7);
+        const uint32_t w01 = (dw & 1) ? a.y : a.x;
+        const uint32_t w23 = (dw & 1) ? a.w : a.z;
+        const uint32_t wv = (dw & 2) ? w23 : w01;
+        const int pos = Q.n + mbcnt(mk);
+        Q.lab[pos] = static_cast<int>(tile_base + i0 + dw * 4 + byte);
+        Q.m[pos] = static_cast<int>((wv >> (byte * 8)) & 0xFFu);
+      }
+      Q.n += __popcll(mk);
+      if (Q.n >= kWave) flush<KPL>(p, Q, top, kWave, gx, -1.0, lane);
+    }
+  };
+#pragma unroll 1
+  for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4 * 4) {
+    uint4 a[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a[i] = *reinterpret_cast<const uint4*>(acc + b0 + i * kWave * 4 + lane * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) block(a[i], (b0 >> 8) + i);
+  }
+}
+
+// Venues 64.. of a row with more than 64 venues: their buckets of tile t,
+// loaded and scattered synchronously (pass `pass` of mode lnp).
+__device__ __forceinline__ void extra_groups(const CctParams& p, const Stage& S, uint32_t* acc,
+                                             int64_t pb, int d, int lane) {
+  for (int g0 = kWave; g0 < d; g0 += kWave) {
+    const int j = g0 + lane;
+    uint32_t lo = 0, hi = 0;
+    int c = 0;
+    if (j < d) {
+      const uint32_t b = static_cast<uint32_t>(p.c_col[pb + j]) * static_cast<uint32_t>(p.T) +
+                         static_cast<uint32_t>(S.t);
+      lo = p.tile_off[b];
+      hi = p.tile_off[b + 1];
+      c = p.c_val[pb + j];
+    }
+    Stage E = S;
+    grp_set(E.G, lo, hi, c, d - g0 < kWave ? d - g0 : kWave);
+    E.nb = (E.G.nq + kWave * kU - 1) / (kWave * kU);
+    for (int b = 0; b < E.nb; ++b) {
+      Batch B;
+      issue<1>(E, b, p.tile_ent, 0, lane, B, false);
+      scatter_any<true>(B, E, acc, 0u, kLabMask1, kS1);
+    }
+  }
+}
+
+template <int KPL>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_cct1(CctParams p) {
+  // LDS: the accumulator at address 0 (scatter ORs the in-tile offset into 0)
+  // then the candidate queue.
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* acc = lds;
+  const int lane = lane_id();
+  CandQ Q;
+  Q.lab = reinterpret_cast<int*>(lds + kAcc1);
+  Q.m = Q.lab + kQ;
+  Q.n = 0;
+  for (int i = lane * 4; i < kAcc1; i += kWave * 4)
+    *reinterpret_cast<uint4*>(acc + i) = make_uint4(0, 0, 0, 0);
+
+  for (;;) {
+    unsigned long long rr = 0;
+    if (lane == 0) rr = atomicAdd(p.counter, 1ull);
+    const int64_t r = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rr)));
+    if (r >= p.n_rows) break;
+    const int64_t x = p.row_order ? static_cast<int64_t>(p.row_order[r]) : p.row_begin + r;
+    const bool is_piece = r < p.n_pieces;
+    const int64_t ro = (is_piece || p.out_by_slot) ? r : x - p.row_begin;
+    const int t_beg = is_piece ? p.piece_t0[r] : 0;
+    const int t_end = is_piece ? p.piece_t1[r] : static_cast<int>(p.T);
+    DPS_DASSERT(0 <= t_beg && t_beg <= t_end && t_end <= p.T);
+    const int64_t x_lab = p.t_rank ? static_cast<int64_t>(p.t_rank[x]) : x;
+    const int64_t pb = p.c_ptr[x];
+    const int d = static_cast<int>(p.c_ptr[x + 1] - pb);
+    const int64_t gx = p.g[x];
+    const float gxf = i64_f32(gx);
+    TopK<KPL> top;
+    top.init(p.k);
+
+    if (d > 0 && t_beg < t_end) {
+      const int d0 = d < kWave ? d : kWave;
+      int c = 0;
+      uint32_t vT = 0;
+      if (lane < d0) {
+        c = p.c_val[pb + lane];
+        vT = static_cast<uint32_t>(p.c_col[pb + lane]) * static_cast<uint32_t>(p.T);
+      }
+      Win1 w;
+      win_load(p, w, t_beg, t_beg, t_end, pb, d, c, vT, lane, -1.0, gxf);
+      uint32_t ub_t = 0;
+      const int t0 = next_tile(p, w, t_end, pb, d, c, vT, lane, -1.0, gxf, ub_t);
+      if (t0 >= 0) {
+        Pend1 P;
+        pend_load(p, P, t0, ub_t, d0, vT, lane);
+        Stage1 X;
+        stage_make(X, P, c, d0);
+        Batch B;
+        issue<1>(X.S, 0, p.tile_ent, 0, lane, B, false);
+        const int t1 = next_tile(p, w, t_end, pb, d, c, vT, lane, -1.0, gxf, ub_t);
+        pend_load(p, P, t1, ub_t, d0, vT, lane);
+        for (;;) {
+          const int npass = 1 << X.S.lnp;
+          bool more = false;
+          for (X.S.pass = 0; X.S.pass < npass; ++X.S.pass) {
+            if (X.S.pass > 0) issue<1>(X.S, 0, p.tile_ent, 0, lane, B, false);
+            scatter_any<true>(B, X.S, acc, 0u, kLabMask1, kS1);
+            for (int b = 1; b < X.S.nb; ++b) {
+              Batch B2;
+              issue<1>(X.S, b, p.tile_ent, 0, lane, B2, false);
+              scatter_any<true>(B2, X.S, acc, 0u, kLabMask1, kS1);
+            }
+            if (d > kWave) extra_groups(p, X.S, acc, pb, d, lane);
+            // score what is queued while the list is filling or the queue is
+            // half full (one memory round trip per 64 candidates)
+            if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
+              flush<KPL>(p, Q, top, Q.n, gx, -1.0, lane);
+            const double tau = top.full() ? top.kth_s : -1.0;
+            int mseg = 1;
+            if (tau > 0.0) {
+              const int mn = mneed_lo32(static_cast<float>(tau), gxf + X.gsf);
+              mseg = mn > 1 ? mn : 1;
+            }
+            const bool last = X.S.pass + 1 == npass;
+            Stage S = X.S;
+            if (last) {
+              // next stage: its bounds were loaded one stage ago; put its first
+              // chunks in flight, then load the bounds of the one after
+              if (tau > w.tau) {
+                w.live &= win_pass(w, tau, gxf);
+                w.tau = tau;
+              }
+              more = P.t >= 0;
+              if (more) stage_make(X, P, c, d0);
+              else X.S.G.nq = 0;
+              issue<1>(X.S, 0, p.tile_ent, 0, lane, B, false);
+              const int tn = more ? next_tile(p, w, t_end, pb, d, c, vT, lane, tau, gxf, ub_t) : -1;
+              pend_load(p, P, tn, ub_t, d0, vT, lane);
+            }
+            if (S.lnp == 0) {
+              epi1_u8<KPL>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg);
+            } else {
+              epilogue<KPL, 1>(p, acc, top, Q, S, 0, lane, kAcc1, kSeg1, x_lab, gx, -1.0, mseg);
+            }
+            if (last) break;
+          }
+          if (!more) break;
+        }
+      }
+    }
+    if (Q.n > 0) flush<KPL>(p, Q, top, Q.n, gx, -1.0, lane);
+
+    // ranked entries, then zero-score targets in reference order, then -1
+    int32_t* oi = (is_piece ? p.piece_idx : p.out_idx) + ro * p.k;
+    int64_t* oc = (is_piece ? p.piece_cnt : p.out_cnt) + ro * p.k;
+    double* os = (is_piece ? p.piece_score : p.out_score) + ro * p.k;
+#pragma unroll
+    for (int q = 0; q < KPL; ++q) {
+      const int slot = q * kWave + lane;
+      if (slot < top.filled) { oi[slot] = top.y[q]; oc[slot] = top.m[q]; os[slot] = top.s[q]; }
+    }
+    const int64_t avail = p.n_targets - 1;
+    const int want = is_piece ? top.filled : static_cast<int>(avail < p.k ? avail : p.k);
+    int slot = top.filled;
+    for (int64_t yb = 0; slot < want && yb < p.n_targets; yb += kWave) {
+      const int64_t yc = yb + lane;
+      bool ok = yc < p.n_targets && yc != x;
+      for (int q = 0; q < KPL; ++q) {
+        for (int l = 0; l < kWave; ++l) {
+          if (q * kWave + l >= top.filled) break;
+          ok = ok && (readlane(top.y[q], l) != static_cast<int>(yc));
+        }
+      }
+      const uint64_t mk = ballot(ok);
+      const int rank = mbcnt(mk);
+      if (ok && slot + rank < want) {
+        oi[slot + rank] = static_cast<int32_t>(yc);
+        oc[slot + rank] = 0;
+        os[slot + rank] = 0.0;
+      }
+      slot += __popcll(mk);
+    }
+    for (int s2 = want + lane; s2 < p.k; s2 += kWave) {
+      oi[s2] = -1;
+      oc[s2] = 0;
+      os[s2] = 0.0;
+    }
+  }
+}
+
+template <int KPL>
+int launch1(const CctParams& p, hipStream_t st) {
+  const size_t lds = (static_cast<size_t>(kAcc1) + 2 * kQ) * sizeof(uint32_t);
+  DPS_HIP_RET(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cct1<KPL>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
+  int dev = 0, n_cu = 256;
+  DPS_HIP_RET(hipGetDevice(&dev));
+  DPS_HIP_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  int64_t grid = static_cast<int64_t>(n_cu) * 16;   // 4 waves per SIMD
+  if (grid > p.n_rows) grid = p.n_rows;
+  k_cct1<KPL><<<static_cast<unsigned>(grid), kWave, lds, st>>>(p);
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+}  // namespace
+
+// Lean kernel for W = 8192 (shift 13), one wave per row; the caller has
+// validated the parameters and zeroed p.counter.
+int cct1_launch(const CctParams& p, hipStream_t st) {
+  if (p.shift != kS1) return DPS_ERR_INVALID;
+  if (p.k <= 64) return launch1<1>(p, st);
+  if (p.k <= 128) return launch1<2>(p, st);
+  return launch1<4>(p, st);
+}
+
+}  // namespace dps
