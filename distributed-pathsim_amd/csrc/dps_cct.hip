@@ -578,7 +578,7 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : sizeof(unsigned long long), st));
   // the bench shape (W = 8192, one wave per row) runs the lean kernel
   // (dps_cct1.hip); DPATHSIM_LEAN=0 selects this file's general kernel
-  bool lean = shift == 13 && nw == 1 && p.ablate == 0;
+  bool lean = shift == 13 && nw == 1 && (p.ablate == 0 || p.ablate == 16);
   if (const char* e = std::getenv("DPATHSIM_LEAN")) lean = lean && std::atoi(e) != 0;
   if (lean) return cct1_launch(p, st);
   if (shift <= 13) return dispatch<true>(p, nw, k, st);   // 16-bit tile entries

@@ -153,6 +153,20 @@ __device__ __forceinline__ uint32_t ge_u8_lo(uint32_t a, uint32_t kA) {
   return (a | ((a & 0x7F7F7F7Fu) + kA)) & 0x80808080u;
 }
 
+// Order the row's first 64 venues by their total bucket size, smallest first,
+// so a stage's small buckets sit together at the front of the flattened chunk
+// range (one vector load) and the large ones fill whole fast loads.
+__device__ __forceinline__ void sort_venues(const CctParams& p, int d0, int lane, int& c, uint32_t& vT) {
+  int key = INT_MAX;
+  if (lane < d0) {
+    const uint32_t n = p.tile_off[vT + static_cast<uint32_t>(p.T)] - p.tile_off[vT];
+    key = static_cast<int>((n < (1u << 24) ? n : (1u << 24) - 1u) << 6) | lane;
+  }
+  const int src = wave_bitonic_sort(key) & (kWave - 1);
+  c = __shfl(c, src, kWave);
+  vT = static_cast<uint32_t>(__shfl(static_cast<int>(vT), src, kWave));
+}
+
 // u8 epilogue over the whole tile: 8 blocks of 1024 targets (one threshold
 // segment each, lane l reads dwords 4l..4l+3 of the block), read and zeroed 4
 // at a time; candidates are queued and scored 64 at a time by flush().
@@ -219,6 +233,52 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
   }
 }
 
+// Issue the loads of batch b of stage S (one wave, NW = 1): chunk q -> lane
+// q mod 64, kU loads of 64 consecutive chunks.  The venues owning a load's first
+// and last chunk come from two ballots; a load inside one venue has a scalar
+// base and C.  Boundaries inside a load are resolved without LDS round trips:
+// up to kSel of them by a per-boundary select over readlane'd scalars, more by
+// counting the boundaries each lane has passed and fetching base and C from
+// that venue's lane with two independent bpermutes.
+constexpr int kSel = 8;
+
+__device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __restrict__ ent,
+                                       int lane, Batch& B) {
+  const bool vl = lane < S.G.nv;
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int q0 = b * (kWave * kU) + u * kWave;   // wave-uniform
+    B.c[u] = 0;
+    B.e[u] = make_uint4(0, 0, 0, 0);
+    if (q0 >= S.G.nq) continue;
+    const int q = q0 + lane;
+    const bool live = q < S.G.nq;
+    const int qlast = min(q0 + kWave - 1, S.G.nq - 1);
+    const int jlo = __popcll(ballot(vl && S.G.pre <= q0)) - 1;
+    const int jhi = __popcll(ballot(vl && S.G.pre <= qlast)) - 1;
+    uint32_t bj = readlane(S.G.base, jlo);
+    int cj = readlane(S.G.c, jlo);
+    if (jhi > jlo) {
+      if (jhi - jlo <= kSel) {
+        for (int j = jlo + 1; j <= jhi; ++j) {   // wave-uniform loop
+          const bool ge = q >= readlane(S.G.pre, j);
+          const uint32_t bn = readlane(S.G.base, j);
+          const int cn = readlane(S.G.c, j);
+          bj = ge ? bn : bj;
+          cj = ge ? cn : cj;
+        }
+      } else {
+        int j = jlo;
+        for (int jj = jlo + 1; jj <= jhi; ++jj) j += q >= readlane(S.G.pre, jj) ? 1 : 0;
+        bj = static_cast<uint32_t>(__shfl(static_cast<int>(S.G.base), j, kWave));
+        cj = __shfl(S.G.c, j, kWave);
+      }
+    }
+    B.e[u] = *reinterpret_cast<const uint4*>(ent + (live ? bj + 4u * static_cast<uint32_t>(q) : 0u));
+    B.c[u] = live ? cj : 0;
+  }
+}
+
 // Venues 64.. of a row with more than 64 venues: their buckets of tile t,
 // loaded and scattered synchronously (pass `pass` of mode lnp).
 __device__ __forceinline__ void extra_groups(const CctParams& p, const Stage& S, uint32_t* acc,
@@ -239,7 +299,7 @@ __device__ __forceinline__ void extra_groups(const CctParams& p, const Stage& S,
     E.nb = (E.G.nq + kWave * kU - 1) / (kWave * kU);
     for (int b = 0; b < E.nb; ++b) {
       Batch B;
-      issue<1>(E, b, p.tile_ent, 0, lane, B, false);
+      issue1(E, b, p.tile_ent, lane, B);
       scatter_any<true>(B, E, acc, 0u, kLabMask1, kS1);
     }
   }
@@ -258,6 +318,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
   Q.n = 0;
   for (int i = lane * 4; i < kAcc1; i += kWave * 4)
     *reinterpret_cast<uint4*>(acc + i) = make_uint4(0, 0, 0, 0);
+  // profiling aid (-DDPS_PROFILE build, DPATHSIM_ABLATE=16): shader-clock
+  // cycles per phase (scatter, flush + thresholds, next-stage prefetch,
+  // epilogue) and the stage count, summed over waves into counter[8..12]
+  const bool prof = kProfile && (p.ablate & 16) != 0;
+  uint64_t ts[7] = {0, 0, 0, 0, 0, 0, 0}, pc[7] = {0, 0, 0, 0, 0, 0, 0};
 
   for (;;) {
     unsigned long long rr = 0;
@@ -286,6 +351,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         c = p.c_val[pb + lane];
         vT = static_cast<uint32_t>(p.c_col[pb + lane]) * static_cast<uint32_t>(p.T);
       }
+      if (d0 > 1) sort_venues(p, d0, lane, c, vT);
       Win1 w;
       win_load(p, w, t_beg, t_beg, t_end, pb, d, c, vT, lane, -1.0, gxf);
       uint32_t ub_t = 0;
@@ -296,21 +362,23 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         Stage1 X;
         stage_make(X, P, c, d0);
         Batch B;
-        issue<1>(X.S, 0, p.tile_ent, 0, lane, B, false);
+        issue1(X.S, 0, p.tile_ent, lane, B);
         const int t1 = next_tile(p, w, t_end, pb, d, c, vT, lane, -1.0, gxf, ub_t);
         pend_load(p, P, t1, ub_t, d0, vT, lane);
         for (;;) {
           const int npass = 1 << X.S.lnp;
           bool more = false;
           for (X.S.pass = 0; X.S.pass < npass; ++X.S.pass) {
-            if (X.S.pass > 0) issue<1>(X.S, 0, p.tile_ent, 0, lane, B, false);
+            if (prof) ts[0] = __builtin_amdgcn_s_memtime();
+            if (X.S.pass > 0) issue1(X.S, 0, p.tile_ent, lane, B);
             scatter_any<true>(B, X.S, acc, 0u, kLabMask1, kS1);
             for (int b = 1; b < X.S.nb; ++b) {
               Batch B2;
-              issue<1>(X.S, b, p.tile_ent, 0, lane, B2, false);
+              issue1(X.S, b, p.tile_ent, lane, B2);
               scatter_any<true>(B2, X.S, acc, 0u, kLabMask1, kS1);
             }
             if (d > kWave) extra_groups(p, X.S, acc, pb, d, lane);
+            if (prof) ts[1] = __builtin_amdgcn_s_memtime();
             // score what is queued while the list is filling or the queue is
             // half full (one memory round trip per 64 candidates)
             if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
@@ -323,6 +391,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
             }
             const bool last = X.S.pass + 1 == npass;
             Stage S = X.S;
+            if (prof) ts[2] = __builtin_amdgcn_s_memtime();
             if (last) {
               // next stage: its bounds were loaded one stage ago; put its first
               // chunks in flight, then load the bounds of the one after
@@ -333,14 +402,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
               more = P.t >= 0;
               if (more) stage_make(X, P, c, d0);
               else X.S.G.nq = 0;
-              issue<1>(X.S, 0, p.tile_ent, 0, lane, B, false);
+              if (prof) ts[5] = __builtin_amdgcn_s_memtime();
+              issue1(X.S, 0, p.tile_ent, lane, B);
+              if (prof) ts[6] = __builtin_amdgcn_s_memtime();
               const int tn = more ? next_tile(p, w, t_end, pb, d, c, vT, lane, tau, gxf, ub_t) : -1;
               pend_load(p, P, tn, ub_t, d0, vT, lane);
             }
+            if (prof) ts[3] = __builtin_amdgcn_s_memtime();
             if (S.lnp == 0) {
               epi1_u8<KPL>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg);
             } else {
               epilogue<KPL, 1>(p, acc, top, Q, S, 0, lane, kAcc1, kSeg1, x_lab, gx, -1.0, mseg);
+            }
+            if (prof) {
+              ts[4] = __builtin_amdgcn_s_memtime();
+#pragma unroll
+              for (int i = 0; i < 4; ++i) pc[i] += ts[i + 1] - ts[i];
+              ++pc[4];
+              if (last) { pc[5] += ts[5] - ts[2]; pc[6] += ts[6] - ts[5]; }
             }
             if (last) break;
           }
@@ -385,6 +464,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
       oc[s2] = 0;
       os[s2] = 0.0;
     }
+  }
+  if (prof && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) atomicAdd(p.counter + 8 + i, static_cast<unsigned long long>(pc[i]));
   }
 }
 

@@ -1,0 +1,24 @@
+"""Phase cycles of the lean hot kernel (profiling build, DPATHSIM_ABLATE=16):
+shader-clock cycles per wave-stage in scatter / flush+thresholds / next-stage
+prefetch / epilogue, on the full config3 launch."""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "distributed-pathsim_amd"))
+import torch
+from dpathsim.synth import synth_config
+from dpathsim.engine import build_engine
+
+eng = build_engine(synth_config(os.environ.get("AB_CONFIG", "config3")).typed(), tile_w=8192)
+R = eng.typed.n_authors
+for ab in ("0", "16"):
+    os.environ["DPATHSIM_ABLATE"] = ab
+    eng.topk(10, 0, 20000); torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(); eng.topk(10, 0, R); e1.record(); torch.cuda.synchronize()
+    print(f"ablate {ab}: {e0.elapsed_time(e1):.2f} ms", flush=True)
+c = eng.tensor("topk_ws")[:256].view(torch.int64).cpu().tolist()
+st = max(c[12], 1)
+names = ["scatter", "flush+thresholds", "prefetch", "epilogue"]
+tot = sum(c[8:12])
+print(f"  prefetch split: refilter+stage_make {c[13] / st:.0f}, issue batch 0 {c[14] / st:.0f}, rest {(c[10] - c[13] - c[14]) / st:.0f}", flush=True)
+print(f"stages {st} ({st / R:.1f} per row); cycles per wave-stage: " +
+      " ".join(f"{n} {c[8 + i] / st:.0f} ({c[8 + i] / tot:.0%})" for i, n in enumerate(names)), flush=True)
