@@ -23,6 +23,11 @@
 // Skipping a tile is sound for the same reason as in k_cct_topk: UB bounds
 // every M of the tile and mneed_lo32(tau, gx + gmin_t) is at most the
 // smallest M whose score can reach tau (ties included).
+// Three 64-chunk loads per batch (not the general kernel's four): with the
+// candidate queue in VGPRs it keeps the kernel within 96 VGPRs, 5 waves per SIMD.
+#ifndef DPS_KU
+#define DPS_KU 3
+#endif
 #include "dps_cct_dev.hpp"
 
 #include <cstdlib>
@@ -35,6 +40,10 @@ constexpr int kW1 = 1 << kS1;                 // 8192 targets per tile
 constexpr int kAcc1 = kW1 / 4;                // accumulator dwords (packed u8)
 constexpr int kSeg1 = 10;                     // threshold segments of 1024 targets
 constexpr uint32_t kLabMask1 = (kW1 - 1) & ~3u;
+#ifndef DPS_EPI1
+#define DPS_EPI1 2
+#endif
+constexpr int kEpi1 = DPS_EPI1;                // epilogue blocks read per trip
 
 // 64 consecutive tiles of one row: lane l describes tile w0 + l.
 struct Win1 {
@@ -167,11 +176,101 @@ __device__ __forceinline__ void sort_venues(const CctParams& p, int d0, int lane
   vT = static_cast<uint32_t>(__shfl(static_cast<int>(vT), src, kWave));
 }
 
+// Candidate queue in VGPRs (no LDS: the wave's 8 KB of LDS is all
+// accumulator, so 20 waves fit a CU): slot s lives in lane s % 64, register
+// s / 64.  Appends come 64 lanes at a time while n < 64, so n < 128.
+struct VQ {
+  int lab0, m0;   // slots 0..63
+  int lab1, m1;   // slots 64..127
+  int n;          // wave-uniform fill
+};
+
+// Append the candidates of the lanes in mk (this lane's (lab, m) if set) at
+// slots n, n + 1, ...: a forward permute sends each to lane slot % 64; lanes
+// without a candidate send theirs to a lane outside the receiving window.
+__device__ __forceinline__ void vq_push(VQ& Q, bool has, int lab, int m, uint64_t mk, int lane) {
+  const int cnt = __popcll(mk);
+  const int pos = Q.n + mbcnt(mk);
+  const int dst = has ? (pos & (kWave - 1)) : ((Q.n - 1) & (kWave - 1));
+  const int plab = __builtin_amdgcn_ds_permute(dst << 2, lab);
+  const int pm = __builtin_amdgcn_ds_permute(dst << 2, m);
+  const bool recv = cnt >= kWave || ((lane - Q.n) & (kWave - 1)) < cnt;
+  const bool hi = lane < Q.n;                     // wrapped past slot 63
+  if (recv && !hi) { Q.lab0 = plab; Q.m0 = pm; }
+  if (recv && hi) { Q.lab1 = plab; Q.m1 = pm; }
+  Q.n += cnt;
+}
+
+// Exact score of the first n (<= 64) queued candidates; insert those that beat
+// the k-th entry; drop them from the queue (n == 64 moves slots 64.. down).
+template <int KPL>
+__device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& top, int n,
+                                         int64_t gx, int lane) {
+  bool cand = lane < n;
+  int M = 0, yo = 0;
+  double sc = 0.0;
+  if (cand) {
+    const int64_t label = Q.lab0;
+    M = Q.m0;
+    yo = p.t_perm ? p.t_perm[label] : static_cast<int>(label);
+    const int64_t den = gx + p.g_t[label];
+    sc = static_cast<double>(2 * static_cast<int64_t>(M)) / static_cast<double>(den);
+    cand = better(sc, yo, top.kth_s, top.kth_y);
+  }
+  if (n >= kWave) { Q.lab0 = Q.lab1; Q.m0 = Q.m1; }
+  Q.n -= n;
+  uint64_t mask = ballot(cand);
+  while (mask) {
+    const int srcl = __ffsll(static_cast<long long>(mask)) - 1;
+    mask &= mask - 1;
+    const double cs = readlane(sc, srcl);
+    const int cy = readlane(yo, srcl);
+    if (!better(cs, cy, top.kth_s, top.kth_y)) continue;
+    top.insert(cs, cy, readlane(M, srcl));
+  }
+}
+
+// u16 / u32 pass epilogue (UB > 255, rare): scan + zero the accumulator of
+// pass `pass` (2 or 1 targets per dword), queue targets reaching their
+// segment's threshold.
+template <int KPL>
+__device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
+                                          const Stage& S, int lane, int64_t x_lab, int64_t gx,
+                                          int mseg) {
+  const int lnp = S.lnp;
+  const int tpd_shift = 2 - lnp;                     // log2(targets per dword)
+  const int bits = 8 << lnp;
+  const uint32_t vmask = lnp == 2 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
+  const int64_t tile_base = S.t << kS1;
+  const int pass_base = S.pass << (kS1 - lnp);
+  for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4) {
+    const int b = b0 + lane * 4;
+    const uint4 a = *reinterpret_cast<const uint4*>(acc + b);
+    *reinterpret_cast<uint4*>(acc + b) = make_uint4(0, 0, 0, 0);
+    const int i0 = pass_base + (b << tpd_shift);     // first target of this lane's 16 bytes
+    const uint32_t m = static_cast<uint32_t>(__shfl(mseg, (i0 >> kSeg1) & (kWave - 1), kWave));
+    const bool any = block_any(a, m, lnp);
+    if (!ballot(any)) continue;
+#pragma unroll 1
+    for (int v = 0; v < (16 >> lnp); ++v) {
+      const int di = v >> tpd_shift;
+      const uint32_t wv = di == 0 ? a.x : di == 1 ? a.y : di == 2 ? a.z : a.w;
+      const uint32_t M = (wv >> ((v & ((1 << tpd_shift) - 1)) * bits)) & vmask;
+      const int64_t label = tile_base + i0 + v;
+      const bool cand = any && M >= m && label != x_lab;
+      const uint64_t mk = ballot(cand);
+      if (!mk) continue;
+      vq_push(Q, cand, static_cast<int>(label), static_cast<int>(M), mk, lane);
+      if (Q.n >= kWave) vq_flush<KPL>(p, Q, top, kWave, gx, lane);
+    }
+  }
+}
+
 // u8 epilogue over the whole tile: 8 blocks of 1024 targets (one threshold
 // segment each, lane l reads dwords 4l..4l+3 of the block), read and zeroed 4
 // at a time; candidates are queued and scored 64 at a time by flush().
 template <int KPL>
-__device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top, CandQ& Q,
+__device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                         int t, int lane, int64_t x_lab, int64_t gx, int mseg) {
   const int64_t tile_base = static_cast<int64_t>(t) << kS1;
   const int64_t xr = x_lab - tile_base;
@@ -199,11 +298,11 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
       if (rel >= 0 && rel < 16) F &= ~(1u << ((rel & 3) * 8 + 7 - (rel >> 2)));
     }
     if (!ballot(F != 0)) return;
-    wave_lds_fence();
     for (;;) {
       const bool has = F != 0;
       const uint64_t mk = ballot(has);
       if (!mk) break;
+      int lab = 0, mv = 0;
       if (has) {
         const int bit = __builtin_ctz(F);
         F &= F - 1;
@@ -211,25 +310,24 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
         const uint32_t w01 = (dw & 1) ? a.y : a.x;
         const uint32_t w23 = (dw & 1) ? a.w : a.z;
         const uint32_t wv = (dw & 2) ? w23 : w01;
-        const int pos = Q.n + mbcnt(mk);
-        Q.lab[pos] = static_cast<int>(tile_base + i0 + dw * 4 + byte);
-        Q.m[pos] = static_cast<int>((wv >> (byte * 8)) & 0xFFu);
+        lab = static_cast<int>(tile_base + i0 + dw * 4 + byte);
+        mv = static_cast<int>((wv >> (byte * 8)) & 0xFFu);
       }
-      Q.n += __popcll(mk);
-      if (Q.n >= kWave) flush<KPL>(p, Q, top, kWave, gx, -1.0, lane);
+      vq_push(Q, has, lab, mv, mk, lane);
+      if (Q.n >= kWave) vq_flush<KPL>(p, Q, top, kWave, gx, lane);
     }
   };
 #pragma unroll 1
-  for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4 * 4) {
-    uint4 a[4];
+  for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4 * kEpi1) {
+    uint4 a[kEpi1];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < kEpi1; ++i)
       a[i] = *reinterpret_cast<const uint4*>(acc + b0 + i * kWave * 4 + lane * 4);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < kEpi1; ++i)
       *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) block(a[i], (b0 >> 8) + i);
+    for (int i = 0; i < kEpi1; ++i) block(a[i], (b0 >> 8) + i);
   }
 }
 
@@ -306,15 +404,14 @@ __device__ __forceinline__ void extra_groups(const CctParams& p, const Stage& S,
 }
 
 template <int KPL>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_cct1(CctParams p) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL == 1 ? 5 : 4))) void k_cct1(CctParams p) {
   // LDS: the accumulator at address 0 (scatter ORs the in-tile offset into 0)
   // then the candidate queue.
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kAcc1];
   uint32_t* acc = lds;
   const int lane = lane_id();
-  CandQ Q;
-  Q.lab = reinterpret_cast<int*>(lds + kAcc1);
-  Q.m = Q.lab + kQ;
+  VQ Q;
+  Q.lab0 = Q.m0 = Q.lab1 = Q.m1 = 0;
   Q.n = 0;
   for (int i = lane * 4; i < kAcc1; i += kWave * 4)
     *reinterpret_cast<uint4*>(acc + i) = make_uint4(0, 0, 0, 0);
@@ -382,7 +479,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
             // score what is queued while the list is filling or the queue is
             // half full (one memory round trip per 64 candidates)
             if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
-              flush<KPL>(p, Q, top, Q.n, gx, -1.0, lane);
+              vq_flush<KPL>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane);
             const double tau = top.full() ? top.kth_s : -1.0;
             int mseg = 1;
             if (tau > 0.0) {
@@ -412,7 +509,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
             if (S.lnp == 0) {
               epi1_u8<KPL>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg);
             } else {
-              epilogue<KPL, 1>(p, acc, top, Q, S, 0, lane, kAcc1, kSeg1, x_lab, gx, -1.0, mseg);
+              epi1_wide<KPL>(p, acc, top, Q, S, lane, x_lab, gx, mseg);
             }
             if (prof) {
               ts[4] = __builtin_amdgcn_s_memtime();
@@ -427,7 +524,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         }
       }
     }
-    if (Q.n > 0) flush<KPL>(p, Q, top, Q.n, gx, -1.0, lane);
+    while (Q.n > 0) vq_flush<KPL>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane);
 
     // ranked entries, then zero-score targets in reference order, then -1
     int32_t* oi = (is_piece ? p.piece_idx : p.out_idx) + ro * p.k;
@@ -473,15 +570,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 
 template <int KPL>
 int launch1(const CctParams& p, hipStream_t st) {
-  const size_t lds = (static_cast<size_t>(kAcc1) + 2 * kQ) * sizeof(uint32_t);
-  DPS_HIP_RET(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cct1<KPL>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));
   int dev = 0, n_cu = 256;
   DPS_HIP_RET(hipGetDevice(&dev));
   DPS_HIP_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-  int64_t grid = static_cast<int64_t>(n_cu) * 16;   // 4 waves per SIMD
+  int wpc = KPL == 1 ? 20 : 16;   // 5 (k <= 64) or 4 waves per SIMD, 8 KB of LDS each
+  if (const char* e = std::getenv("DPATHSIM_LEAN_WPC")) wpc = std::atoi(e);   // experiments
+  if (wpc < 1 || wpc > 20) wpc = 20;
+  int64_t grid = static_cast<int64_t>(n_cu) * wpc;
   if (grid > p.n_rows) grid = p.n_rows;
-  k_cct1<KPL><<<static_cast<unsigned>(grid), kWave, lds, st>>>(p);
+  k_cct1<KPL><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
   DPS_LAUNCHED();
   return DPS_OK;
 }

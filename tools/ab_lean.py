@@ -18,7 +18,10 @@ NA = eng.typed.n_authors
 R = NA if R <= 0 else min(R, NA)
 res = {}
 for mode in os.environ.get("AB_MODES", "0,1").split(","):
-    os.environ["DPATHSIM_LEAN"] = mode
+    if mode.startswith("w"):   # lean kernel, waves per CU
+        os.environ["DPATHSIM_LEAN_WPC"] = mode[1:]; os.environ["DPATHSIM_LEAN"] = "1"
+    else:
+        os.environ["DPATHSIM_LEAN"] = mode
     eng.topk(k, 0, min(R, 20000)); torch.cuda.synchronize()
     best = 1e30
     for _ in range(reps):
