@@ -28,6 +28,7 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "distributed-pathsim_amd"))
 
+LDS_PEAK_GBS = 256 * 256 * 2.4   # B/clk/CU x CUs x GHz (MI355X_MICROARCH.md LDS)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -144,10 +145,17 @@ def main():
     pairs = NA * (NA - 1)
     value = pairs / (elapsed / args.steps)
 
-    # ---- roofline of the dominant kernel (dps_cct_topk), measured live --------
-    # algorithmic bytes per launch = bytes per C^T entry (16-bit entries up to
-    # tile_w 8192, 32-bit above) x sum_{x in shard} sum_{v in x} n_v entries
-    # read, + the top-k output (20 B per slot) + the row offsets
+    # ---- roofline of the dominant kernel (dps_cct_topk -> k_cct1), measured live --
+    # The kernel is bound by latency at the occupancy LDS capacity allows (5 waves
+    # per SIMD, 8 KB of accumulator each); of the resources it uses the LDS array
+    # is the busiest (PMC, profiles/r02/pmc_hot.json), so the roofline is LDS:
+    # algorithmic LDS bytes per launch = 32 B per 16-byte chunk scattered (8
+    # ds_add_u32 of 4 B per lane) + 16 KiB per accumulator pass (8 KiB read + 8 KiB
+    # zeroed), both counted by the kernel itself (workspace words 1, 2), over the
+    # launch time measured with events on the kernel's stream; peak = 256 B/clk/CU
+    # (ds_read_b128 rate, MI355X_MICROARCH.md LDS) x 256 CUs x 2.4 GHz.
+    # HBM (secondary): 2 B per C^T entry x sum_{x in shard} sum_{v in x} n_v + the
+    # top-k output (20 B per slot) + row offsets, vs 8 TB/s.
     topk_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_topk]))
     r0, r1 = bounds0[rank]
     shard = r1 - r0
@@ -160,8 +168,12 @@ def main():
     terms = int((w[c_ptr[r1]] - w[c_ptr[r0]]).item())      # sum_{x in shard} sum_{v in x} n_v
     ent_bytes = 2 if args.tile_w <= 8192 else 4
     bytes_launch = ent_bytes * terms + 20 * shard * k + 8 * (shard + 1)
-    achieved = bytes_launch / (topk_ms * 1e-3) / 1e9
-    traffic, valu = None, None
+    hbm_achieved = bytes_launch / (topk_ms * 1e-3) / 1e9
+    wsc = eng.tensor("topk_ws")[:24].view(torch.int64).cpu().tolist()   # last launch's counts
+    n_pass, n_chunk = int(wsc[1]), int(wsc[2])
+    lds_bytes = 32 * n_chunk + 16384 * n_pass
+    lds_achieved = lds_bytes / (topk_ms * 1e-3) / 1e9
+    traffic, pmc = None, {}
     if args.pmc_json and os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
@@ -169,9 +181,9 @@ def main():
                     and pm.get("tile_w", args.tile_w) == args.tile_w and args.scale == 1.0
                     and pm.get("k", k) == k and args.denominator == "rowsum"):
                 traffic = pm.get("hbm_bytes_per_launch")
-                valu = pm.get("valu")
+                pmc = {key: pm.get(key) for key in ("lds", "valu", "wait")}
         except Exception:
-            traffic, valu = None, None
+            traffic, pmc = None, {}
     info = eng.info
 
     # ---- secondary rates the north star asks for -----------------------------
@@ -242,13 +254,19 @@ def main():
                        "n_authors": NA, "k": k, "tile_w": args.tile_w,
                        "nnz_C": info.nnz_c, "sum_terms": terms if world == 1 else None,
                        "parallelism": f"row-shard x{world} (work-balanced, heaviest rows first)"},
-            # bound: the resource that binds per the HEAD counters (VALU issue,
-            # see DESIGN.md §5); achieved/peak/frac: algorithmic bytes vs HBM
-            "roofline": {"bound": "valu" if valu else "hbm", "kernel": "dps_cct_topk",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes": bytes_launch, "bytes_per_entry": ent_bytes,
-                         "avg_launch_ms": topk_ms, "valu_issue": valu},
+            # bound: the busiest resource per the HEAD counters (LDS array; the
+            # kernel is latency-bound at the occupancy its LDS allows)
+            "roofline": {"bound": "lds", "kernel": "dps_cct_topk (k_cct1, W 8192)",
+                         "achieved": lds_achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
+                         "frac": lds_achieved / LDS_PEAK_GBS, "traffic": traffic,
+                         "lds_bytes": lds_bytes, "passes": n_pass, "chunks": n_chunk,
+                         "avg_launch_ms": topk_ms,
+                         "pmc": pmc,
+                         "hbm": {"algorithmic_bytes": bytes_launch, "bytes_per_entry": ent_bytes,
+                                 "achieved": hbm_achieved, "peak": HBM_PEAK_GBS,
+                                 "frac": hbm_achieved / HBM_PEAK_GBS,
+                                 "traffic_frac": (traffic / (topk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                                 if traffic else None}},
             "cpu_baseline": cpu,
             "phases_ms": {"cct_topk": topk_ms, "rest_of_step": ms_per_step - topk_ms},
             "spgemm_roofline": spgemm,
