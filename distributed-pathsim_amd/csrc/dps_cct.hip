@@ -575,7 +575,8 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   // ablated run returns wrong top-k lists), the -DDPS_PROFILE build honours it.
   if (kProfile)
     if (const char* ab = std::getenv("DPATHSIM_ABLATE")) p.ablate = std::atoi(ab);
-  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : sizeof(unsigned long long), st));
+  // word 0: row dequeue counter; words 1-2: the lean kernel's pass / chunk counts
+  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : 3 * sizeof(unsigned long long), st));
   // the bench shape (W = 8192, one wave per row) runs the lean kernel
   // (dps_cct1.hip); DPATHSIM_LEAN=0 selects this file's general kernel
   bool lean = shift == 13 && nw == 1 && (p.ablate == 0 || p.ablate == 16);

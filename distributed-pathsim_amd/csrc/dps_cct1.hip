@@ -379,8 +379,9 @@ __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __
 
 // Venues 64.. of a row with more than 64 venues: their buckets of tile t,
 // loaded and scattered synchronously (pass `pass` of mode lnp).
-__device__ __forceinline__ void extra_groups(const CctParams& p, const Stage& S, uint32_t* acc,
-                                             int64_t pb, int d, int lane) {
+__device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, uint32_t* acc,
+                                            int64_t pb, int d, int lane) {
+  int chunks = 0;
   for (int g0 = kWave; g0 < d; g0 += kWave) {
     const int j = g0 + lane;
     uint32_t lo = 0, hi = 0;
@@ -395,12 +396,14 @@ __device__ __forceinline__ void extra_groups(const CctParams& p, const Stage& S,
     Stage E = S;
     grp_set(E.G, lo, hi, c, d - g0 < kWave ? d - g0 : kWave);
     E.nb = (E.G.nq + kWave * kU - 1) / (kWave * kU);
+    chunks += E.G.nq;
     for (int b = 0; b < E.nb; ++b) {
       Batch B;
       issue1(E, b, p.tile_ent, lane, B);
       scatter_any<true>(B, E, acc, 0u, kLabMask1, kS1);
     }
   }
+  return chunks;
 }
 
 template <int KPL>
@@ -420,6 +423,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL == 1 
   // epilogue) and the stage count, summed over waves into counter[8..12]
   const bool prof = kProfile && (p.ablate & 16) != 0;
   uint64_t ts[7] = {0, 0, 0, 0, 0, 0, 0}, pc[7] = {0, 0, 0, 0, 0, 0, 0};
+  // work counts of this wave (wave-uniform), summed into counter[1..2] at exit:
+  // accumulator passes (each reads and zeroes the 8 KiB accumulator) and 16-byte
+  // chunks scattered -- the bench's algorithmic LDS bytes
+  uint64_t n_pass = 0, n_chunk = 0;
 
   for (;;) {
     unsigned long long rr = 0;
@@ -474,7 +481,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL == 1 
               issue1(X.S, b, p.tile_ent, lane, B2);
               scatter_any<true>(B2, X.S, acc, 0u, kLabMask1, kS1);
             }
-            if (d > kWave) extra_groups(p, X.S, acc, pb, d, lane);
+            n_chunk += static_cast<uint64_t>(X.S.G.nq);
+            ++n_pass;
+            if (d > kWave) n_chunk += static_cast<uint64_t>(extra_groups(p, X.S, acc, pb, d, lane));
             if (prof) ts[1] = __builtin_amdgcn_s_memtime();
             // score what is queued while the list is filling or the queue is
             // half full (one memory round trip per 64 candidates)
@@ -561,6 +570,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL == 1 
       oc[s2] = 0;
       os[s2] = 0.0;
     }
+  }
+  if (lane == 0 && (n_pass | n_chunk)) {
+    atomicAdd(p.counter + 1, static_cast<unsigned long long>(n_pass));
+    atomicAdd(p.counter + 2, static_cast<unsigned long long>(n_chunk));
   }
   if (prof && lane == 0) {
 #pragma unroll

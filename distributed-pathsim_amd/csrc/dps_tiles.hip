@@ -204,6 +204,7 @@ constexpr int kBlkLabels = 4096;   // default labels per block (tools/build_ab.p
 // 16 waves per block (one 64-label group each): with 64 KB of LDS per block a
 // CU holds two blocks = 32 waves, enough to cover the latency of the gathers.
 constexpr int kBlkThreads = 1024;
+constexpr int kBlkSub = 8;         // sub-blocks per part
 
 __global__ __launch_bounds__(kBlock) void k_tile_invert(const int32_t* __restrict__ rank,
                                                         int64_t n, int32_t* __restrict__ perm) {
@@ -216,94 +217,256 @@ __device__ __forceinline__ int64_t row_of_label(const int32_t* perm, int64_t lab
   return perm ? static_cast<int64_t>(perm[lab]) : lab;
 }
 
-// The labels of a block are walked 64 at a time per wave (lane = label), and
-// their C entries as one flattened list in 64-entry strips (wave_owner maps a
-// strip slot back to its label), so heavy rows do not serialise one wave.
-struct LabelStrip {
-  int64_t d;       // lane l: c_ptr[y_l] - excl_l (entry index = d_owner + i)
-  uint32_t excl;   // exclusive prefix of the row lengths
-  uint32_t total;  // entries of the 64 labels (wave-uniform)
+// A part (labels_per_block consecutive labels of one tile) is processed by S
+// sub-blocks, each taking an equal share of the part's entries, so the tail
+// part of the highest-g labels -- 8x the mean part's entries, on config3 --
+// no longer sets the kernel time.  A sub-block stages, per label of the part,
+// the exclusive prefix of its row lengths and the row's C offset minus that
+// prefix, then walks its entry range in 64-entry strips with lane = entry:
+// the loads are coalesced, and the LDS atomics of a strip mostly hit distinct
+// venues (the entries of one C row are distinct venues), where per-thread runs
+// through different rows would pile onto the heavy venues' counters.
+struct BlockRows {
+  uint32_t* rel;   // [nl + 1] exclusive prefix of row lengths (LDS)
+  int64_t* d;      // [nl] c_ptr[y] - rel[i] (LDS): entry e of label i is C entry d[i] + e
 };
 
-__device__ __forceinline__ LabelStrip label_strip(const int64_t* __restrict__ c_ptr,
-                                                  const int32_t* __restrict__ perm, int64_t lab,
-                                                  int64_t l1, int64_t* y_out) {
-  int64_t beg = 0;
-  uint32_t len = 0;
-  int64_t y = -1;
-  if (lab < l1) {
-    y = row_of_label(perm, lab);
-    beg = c_ptr[y];
-    len = static_cast<uint32_t>(c_ptr[y + 1] - beg);
+// Stage labels [l0, l1) of the part; returns the part's entry count.  The
+// caller provides LDS for kBlkLabels labels.  g != nullptr: also reduce the
+// part's smallest g into *gmin_s.
+__device__ __forceinline__ uint32_t stage_rows(const int64_t* __restrict__ c_ptr,
+                                               const int32_t* __restrict__ perm,
+                                               const int64_t* __restrict__ g, int64_t l0,
+                                               int64_t l1, BlockRows R, uint32_t* wsum,
+                                               unsigned long long* gmin_s) {
+  const int nl = static_cast<int>(l1 - l0);
+  const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
+  constexpr int kWaves = kBlkThreads / kWave;
+  // pass 1: row lengths (kept in rel[i + 1]) and row offsets
+  unsigned long long gm = ~0ull;
+  constexpr int kPer = kBlkLabels / kBlkThreads;   // labels per thread, loads in flight together
+  int64_t y[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = static_cast<int>(threadIdx.x) + u * kBlkThreads;
+    y[u] = i < nl ? row_of_label(perm, l0 + i) : -1;
   }
-  *y_out = y;
-  const uint32_t inc = wave_inclusive_sum(len);
-  LabelStrip S;
-  S.excl = inc - len;
-  S.total = readlane(inc, kWave - 1);
-  S.d = beg - static_cast<int64_t>(S.excl);
-  return S;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = static_cast<int>(threadIdx.x) + u * kBlkThreads;
+    if (y[u] < 0) continue;
+    const int64_t beg = c_ptr[y[u]];
+    R.rel[i + 1] = static_cast<uint32_t>(c_ptr[y[u] + 1] - beg);
+    R.d[i] = beg;
+    if (g) gm = min(gm, static_cast<unsigned long long>(g[y[u]]));
+  }
+  if (g) {
+    gm = wave_min(gm);
+    if (lane == 0 && gm != ~0ull) atomicMin(gmin_s, gm);
+  }
+  if (threadIdx.x == 0) R.rel[0] = 0;
+  __syncthreads();
+  // pass 2: block-wide inclusive scan of rel[1..nl] in strips of kBlkThreads
+  uint32_t carry = 0;
+  for (int i0 = 0; i0 < nl; i0 += kBlkThreads) {
+    const int i = i0 + static_cast<int>(threadIdx.x);
+    const uint32_t v = i < nl ? R.rel[i + 1] : 0u;
+    const uint32_t inc = wave_inclusive_sum(v);
+    if (lane == kWave - 1) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t off = carry, tot = carry;
+    for (int w = 0; w < kWaves; ++w) {
+      const uint32_t ws = wsum[w];
+      off += w < wave ? ws : 0u;
+      tot += ws;
+    }
+    if (i < nl) {
+      R.rel[i + 1] = off + inc;
+      R.d[i] -= static_cast<int64_t>(off + inc - v);
+    }
+    carry = tot;
+    __syncthreads();
+  }
+  return carry;
 }
 
-// Strip slot i of S: entry index j and owning lane o (all lanes must call).
-__device__ __forceinline__ int64_t strip_entry(const LabelStrip& S, uint32_t i, int* o) {
-  *o = wave_owner(S.excl, i);
-  const int64_t d = __shfl(S.d, *o, kWave);
-  return d + static_cast<int64_t>(i);
+// Strip table of a sub-block: strip k covers entries [e0 + 64k, e0 + 64k + 64)
+// of the part; tab[k] = the label holding its first entry, tab[ns] = the label
+// holding entry e1 - 1, so strip k's labels lie in [tab[k], tab[k + 1]].
+// Built by one pass over the labels (each writes the strip starts it holds).
+constexpr int kMaxStrips = 1024;
+
+__device__ __forceinline__ void strip_table(const BlockRows& R, int nl, uint32_t e0, uint32_t e1,
+                                            int* tab) {
+  const uint32_t ns = (e1 - e0 + kWave - 1) / kWave;
+  for (int i = threadIdx.x; i < nl; i += kBlkThreads) {
+    const uint32_t a = max(R.rel[i], e0), b = min(R.rel[i + 1], e1);
+    if (a >= b) continue;
+    for (uint32_t k = (a - e0 + kWave - 1) / kWave; k < ns && e0 + k * kWave < b; ++k) tab[k] = i;
+    if (e1 - 1 >= a && e1 - 1 < b) tab[ns] = i;
+  }
+  __syncthreads();
 }
 
-// Block (t, h) owns part h of tile t (labels_per_block labels, P parts per
-// tile).  Counting writes the block's per-venue piece counts and maxima to its
-// own slots cntp/mxp[(v*T + t)*P + h] -- no global atomics; k_tile_parts_fix
-// pads each bucket and reduces the maxima, and one exclusive scan over the
-// [v][t][h] order gives every part its base offset, so the scatter needs only
-// LDS cursors.
+// Last label i in [lo, hi] with rel[i] <= e.
+__device__ __forceinline__ int label_at(const uint32_t* rel, int lo, int hi, uint32_t e) {
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (rel[mid] <= e) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Visit entries [e0, e1) of the staged labels in 64-entry strips, lane =
+// entry, kStripU strips per wave at a time (their loads in flight together):
+// fn(label index, venue, C).  A strip's label window comes from the strip
+// table (or, past its capacity, from two wave-uniform searches); each lane then
+// searches only inside it.
+constexpr int kStripU = 4;
+
+template <typename Fn>
+__device__ __forceinline__ void walk_strips(const BlockRows& R, int nl, uint32_t e0, uint32_t e1,
+                                            const int* tab, const int32_t* __restrict__ c_col,
+                                            const int32_t* __restrict__ c_val, Fn&& fn) {
+  const int lane = lane_id();
+  constexpr uint32_t kWaves = kBlkThreads / kWave;
+  const uint32_t ns = (e1 - e0 + kWave - 1) / kWave;
+  for (uint32_t k0 = threadIdx.x / kWave; k0 < ns; k0 += kWaves * kStripU) {
+    int li[kStripU];
+    int64_t j[kStripU];
+#pragma unroll
+    for (int u = 0; u < kStripU; ++u) {
+      const uint32_t k = k0 + u * kWaves;
+      li[u] = -1;
+      j[u] = 0;
+      if (k >= ns) continue;                      // wave-uniform
+      const uint32_t s = e0 + k * kWave;
+      int lo, hi;
+      if (ns <= kMaxStrips) {
+        lo = tab[k];
+        hi = tab[k + 1];
+      } else {
+        lo = label_at(R.rel, 0, nl - 1, s);
+        hi = label_at(R.rel, lo, nl - 1, min(s + kWave - 1u, e1 - 1u));
+      }
+      const uint32_t e = s + static_cast<uint32_t>(lane);
+      if (e < e1) {
+        li[u] = label_at(R.rel, lo, hi, e);
+        j[u] = R.d[li[u]] + e;
+      }
+    }
+    int32_t v[kStripU], c[kStripU];
+#pragma unroll
+    for (int u = 0; u < kStripU; ++u) {
+      v[u] = li[u] >= 0 ? c_col[j[u]] : 0;
+      c[u] = li[u] >= 0 ? c_val[j[u]] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kStripU; ++u)
+      if (li[u] >= 0) fn(li[u], v[u], c[u]);
+  }
+}
+
+// Entries per part (sum of its labels' row lengths), one atomic per wave.
+__global__ __launch_bounds__(kBlock) void k_part_entries(const int64_t* __restrict__ c_ptr,
+                                                         const int32_t* __restrict__ perm,
+                                                         int64_t n_targets, int labels_per_block,
+                                                         uint32_t* __restrict__ part_n) {
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  for (int64_t l0 = wave0 * kWave; l0 < n_targets; l0 += nwaves * kWave) {
+    const int64_t l = l0 + lane_id();
+    uint32_t len = 0;
+    if (l < n_targets) {
+      const int64_t y = row_of_label(perm, l);
+      len = static_cast<uint32_t>(c_ptr[y + 1] - c_ptr[y]);
+    }
+    const uint32_t tot = static_cast<uint32_t>(readlane(static_cast<int>(wave_inclusive_sum(len)), kWave - 1));
+    if (lane_id() == 0 && tot) atomicAdd(&part_n[l0 / labels_per_block], tot);
+  }
+}
+
+// Sub-block sb of a part with n entries: its share [e0, e1) and the part's
+// number of active sub-blocks (n / kSubEntries, at least 1, at most S).
+constexpr uint32_t kSubEntries = 32768;
+struct SubRange {
+  uint32_t e0, e1;
+  int n_sub;
+};
+__device__ __forceinline__ SubRange sub_range(uint32_t n, uint32_t sb, int S) {
+  int n_sub = static_cast<int>((n + kSubEntries - 1) / kSubEntries);
+  n_sub = n_sub < 1 ? 1 : n_sub > S ? S : n_sub;
+  SubRange r;
+  r.n_sub = n_sub;
+  r.e0 = static_cast<uint32_t>(static_cast<uint64_t>(n) * sb / n_sub);
+  r.e1 = static_cast<uint32_t>(static_cast<uint64_t>(n) * (sb + 1) / n_sub);
+  return r;
+}
+
+// Part p = (t, h) of tile t (labels_per_block labels, P parts per tile),
+// sub-block sb of up to S (sub_range: one per kSubEntries entries of the part).
+// Counting writes the sub-block's per-venue piece counts and maxima into the
+// part's slots cntp/mxp[(v*T + t)*P + h] -- plain stores when the part has one
+// active sub-block, one global atomic per (sub-block, venue) otherwise;
+// k_tile_parts_fix pads each bucket and reduces the maxima, and one exclusive
+// scan over the [v][t][h] order gives every part its base offset.
 __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
     const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
     const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm,
     const int64_t* __restrict__ g, int64_t n_targets, int64_t n_mids, int shift, int64_t T,
-    int labels_per_block, int P, uint32_t* __restrict__ cntp, uint32_t* __restrict__ mxp,
+    int labels_per_block, int P, int S, const uint32_t* __restrict__ part_n,
+    uint32_t* __restrict__ cntp, uint32_t* __restrict__ mxp,
     unsigned long long* __restrict__ gmin, int32_t* __restrict__ status) {
   __shared__ uint32_t cnt_s[kBlkMids];
   __shared__ uint32_t mx_s[kBlkMids];
+  __shared__ uint32_t rel_s[kBlkLabels + 1];
+  __shared__ int64_t d_s[kBlkLabels];
+  __shared__ int tab_s[kMaxStrips + 1];
+  __shared__ uint32_t wsum[kBlkThreads / kWave];
   __shared__ unsigned long long gmin_s;
+  __shared__ int ovf_s;
+  // sub-block major (block = sb * n_parts + part): the parts' first sub-blocks
+  // -- the only ones most parts use -- spread over every XCD
+  const int64_t n_parts = gridDim.x / S;
+  const int64_t part = blockIdx.x % n_parts;
+  const uint32_t sb = static_cast<uint32_t>(blockIdx.x / n_parts);
+  const SubRange sr = sub_range(part_n[part], sb, S);
+  if (static_cast<int>(sb) >= sr.n_sub) return;   // block-uniform: before any barrier
   for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) { cnt_s[v] = 0; mx_s[v] = 0; }
-  if (threadIdx.x == 0) gmin_s = ~0ull;
-  __syncthreads();
-  const int lane = lane_id();
-  const int wave = threadIdx.x / kWave;
+  if (threadIdx.x == 0) { gmin_s = ~0ull; ovf_s = 0; }
   const bool p16 = shift <= kP16MaxShift;
-  const int64_t l0 = static_cast<int64_t>(blockIdx.x) * labels_per_block;
+  const int64_t l0 = part * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
   const int64_t t = l0 >> shift;
-  const int64_t h = static_cast<int64_t>(blockIdx.x) % P;
-  unsigned long long gm = ~0ull;
-  for (int64_t lb = l0 + wave * kWave; lb < l1; lb += kBlkThreads) {
-    int64_t y;
-    const LabelStrip S = label_strip(c_ptr, perm, lb + lane, l1, &y);
-    if (g && y >= 0) gm = min(gm, static_cast<unsigned long long>(g[y]));
-    for (uint32_t e0 = 0; e0 < S.total; e0 += kWave) {
-      int o;
-      const int64_t j = strip_entry(S, e0 + lane, &o);
-      if (e0 + lane < S.total) {
-        const int32_t c = c_val[j];
-        if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
-        const int32_t v = c_col[j];
-        atomicAdd(&cnt_s[v], n_pieces(p16, static_cast<uint32_t>(c),
-                                      static_cast<uint32_t>(lb + o)));
-        atomicMax(&mx_s[v], static_cast<uint32_t>(c));
-      }
-    }
-  }
-  gm = wave_min(gm);
-  if (lane == 0 && gm != ~0ull) atomicMin(&gmin_s, gm);
+  const int64_t h = part % P;
   __syncthreads();
+  const BlockRows R{rel_s, d_s};
+  const int nl = static_cast<int>(l1 - l0);
+  const bool do_g = gmin && sb == 0;
+  const uint32_t n = stage_rows(c_ptr, perm, do_g ? g : nullptr, l0, l1, R, wsum, &gmin_s);
+  DPS_DASSERT(n == part_n[part]);
+  if (sr.e1 - sr.e0 <= kMaxStrips * kWave) strip_table(R, nl, sr.e0, sr.e1, tab_s);
+  const uint32_t lab0 = static_cast<uint32_t>(l0);
+  walk_strips(R, nl, sr.e0, sr.e1, tab_s, c_col, c_val, [&](int i, int32_t v, int32_t c) {
+    if (c > 0xFFFF) ovf_s = 1;
+    atomicAdd(&cnt_s[v], n_pieces(p16, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
+    atomicMax(&mx_s[v], static_cast<uint32_t>(c));
+  });
+  __syncthreads();
+  if (threadIdx.x == 0 && ovf_s && status) *status = DPS_ERR_OVERFLOW;
   for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) {
     if (!cnt_s[v]) continue;
-    cntp[(v * T + t) * P + h] = cnt_s[v];
-    mxp[(v * T + t) * P + h] = mx_s[v];
+    const int64_t slot = (v * T + t) * P + h;
+    if (sr.n_sub == 1) {
+      cntp[slot] = cnt_s[v];
+      mxp[slot] = mx_s[v];
+    } else {
+      atomicAdd(&cntp[slot], cnt_s[v]);
+      atomicMax(&mxp[slot], mx_s[v]);
+    }
   }
-  if (threadIdx.x == 0 && gmin && gmin_s != ~0ull) atomicMin(&gmin[t], gmin_s);
+  if (threadIdx.x == 0 && do_g && gmin_s != ~0ull) atomicMin(&gmin[t], gmin_s);
 }
 
 // Per bucket b: tot = real entries (kept in cnt[b] for the padding pass),
@@ -326,37 +489,65 @@ __global__ __launch_bounds__(kBlock) void k_tile_parts_fix(uint32_t* __restrict_
   }
 }
 
+// Scatter: a part with one active sub-block places its entries from the part's
+// base offsets; with several, each sub-block counts its own entries per venue,
+// reserves its range inside every part slot it touches (one global atomic per
+// venue on curp), then places them with 64-bit LDS cursors.
 __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
     const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
     const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm, int64_t n_targets,
-    int64_t n_mids, int shift, int64_t T, int labels_per_block, int P,
-    const int64_t* __restrict__ offp, uint32_t* __restrict__ ent) {
-  __shared__ uint32_t cur_s[kBlkMids];
-  for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) cur_s[v] = 0;
-  __syncthreads();
-  const int lane = lane_id();
-  const int wave = threadIdx.x / kWave;
+    int64_t n_mids, int shift, int64_t T, int labels_per_block, int P, int S,
+    const uint32_t* __restrict__ part_n, const int64_t* __restrict__ offp,
+    uint32_t* __restrict__ curp, uint32_t* __restrict__ ent) {
+  __shared__ uint32_t cnt_s[kBlkMids];
+  __shared__ unsigned long long base_s[kBlkMids];
+  __shared__ uint32_t rel_s[kBlkLabels + 1];
+  __shared__ int64_t d_s[kBlkLabels];
+  __shared__ int tab_s[kMaxStrips + 1];
+  __shared__ uint32_t wsum[kBlkThreads / kWave];
+  // sub-block major (block = sb * n_parts + part): the parts' first sub-blocks
+  // -- the only ones most parts use -- spread over every XCD
+  const int64_t n_parts = gridDim.x / S;
+  const int64_t part = blockIdx.x % n_parts;
+  const uint32_t sb = static_cast<uint32_t>(blockIdx.x / n_parts);
+  const SubRange sr = sub_range(part_n[part], sb, S);
+  if (static_cast<int>(sb) >= sr.n_sub) return;   // block-uniform: before any barrier
+  for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) cnt_s[v] = 0;
   const bool p16 = shift <= kP16MaxShift;
-  const int64_t l0 = static_cast<int64_t>(blockIdx.x) * labels_per_block;
+  const int64_t l0 = part * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
   const int64_t t = l0 >> shift;
-  const int64_t h = static_cast<int64_t>(blockIdx.x) % P;
+  const int64_t h = part % P;
   const uint32_t ymask = (1u << shift) - 1u;
-  for (int64_t lb = l0 + wave * kWave; lb < l1; lb += kBlkThreads) {
-    int64_t y;
-    const LabelStrip S = label_strip(c_ptr, perm, lb + lane, l1, &y);
-    for (uint32_t e0 = 0; e0 < S.total; e0 += kWave) {
-      int o;
-      const int64_t j = strip_entry(S, e0 + lane, &o);
-      if (e0 + lane < S.total) {
-        const int32_t v = c_col[j];
-        const uint32_t c = static_cast<uint32_t>(c_val[j]);
-        const uint32_t lab = static_cast<uint32_t>(lb + o) & ymask;
-        const uint32_t pos = atomicAdd(&cur_s[v], n_pieces(p16, c, lab));
-        put_entry(p16, ent, offp[(v * T + t) * P + h] + pos, c, lab);
-      }
+  __syncthreads();
+  const BlockRows R{rel_s, d_s};
+  const int nl = static_cast<int>(l1 - l0);
+  stage_rows(c_ptr, perm, nullptr, l0, l1, R, wsum, nullptr);
+  if (sr.e1 - sr.e0 <= kMaxStrips * kWave) strip_table(R, nl, sr.e0, sr.e1, tab_s);
+  const uint32_t lab0 = static_cast<uint32_t>(l0) & ymask;
+  if (sr.n_sub == 1) {
+    for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads)
+      base_s[v] = static_cast<unsigned long long>(offp[(v * T + t) * P + h]);
+  } else {
+    walk_strips(R, nl, sr.e0, sr.e1, tab_s, c_col, c_val, [&](int i, int32_t v, int32_t c) {
+      atomicAdd(&cnt_s[v], n_pieces(p16, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
+    });
+    __syncthreads();
+    for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) {
+      const uint32_t nv = cnt_s[v];
+      if (!nv) continue;
+      const int64_t slot = (v * T + t) * P + h;
+      base_s[v] = static_cast<unsigned long long>(offp[slot] + atomicAdd(&curp[slot], nv));
     }
   }
+  __syncthreads();
+  walk_strips(R, nl, sr.e0, sr.e1, tab_s, c_col, c_val, [&](int i, int32_t v, int32_t c) {
+    const uint32_t lab = lab0 + static_cast<uint32_t>(i);
+    const unsigned long long pos =
+        atomicAdd(&base_s[v], static_cast<unsigned long long>(
+                                  n_pieces(p16, static_cast<uint32_t>(c), lab)));
+    put_entry(p16, ent, static_cast<int64_t>(pos), static_cast<uint32_t>(c), lab);
+  });
 }
 
 // --------------------------------------------------------------------------
@@ -458,8 +649,15 @@ int log2_exact(int32_t w) {
 int tile_lpb(int32_t tile_w) {
   int lpb = kBlkLabels;
   if (const char* e = std::getenv("DPATHSIM_TILE_LPB")) lpb = std::atoi(e);
-  if (lpb < 1024 || (lpb & (lpb - 1))) lpb = kBlkLabels;
+  if (lpb < 1024 || lpb > kBlkLabels || (lpb & (lpb - 1))) lpb = kBlkLabels;
   return tile_w < lpb ? tile_w : lpb;
+}
+
+// Sub-blocks per part of the block-local build (entries split evenly).
+int tile_sub() {
+  int sub = kBlkSub;
+  if (const char* e = std::getenv("DPATHSIM_TILE_SUB")) sub = std::atoi(e);
+  return sub < 1 || sub > 64 ? kBlkSub : sub;
 }
 
 // Parts per tile of the block-local build (1 on the global-atomic path).
@@ -524,6 +722,8 @@ size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t ti
   s += align_up(scan_workspace_size(np + 1));
   s += align_up(static_cast<size_t>(np + 1) * sizeof(uint32_t));  // cntp
   s += align_up(static_cast<size_t>(np + 1) * sizeof(uint32_t));  // mxp
+  s += align_up(static_cast<size_t>(np + 1) * sizeof(uint32_t));  // curp
+  s += align_up(static_cast<size_t>(np + 1) * sizeof(uint32_t));  // part_n
   s += align_up(static_cast<size_t>(n_targets > 0 ? n_targets : 1) * sizeof(int32_t));  // perm
   return s + 1024;
 }
@@ -557,10 +757,14 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   void* sws = c.take<char>(scan_ws);
   uint32_t* cntp = c.take<uint32_t>(np + 1);
   uint32_t* mxp = c.take<uint32_t>(np + 1);
+  uint32_t* curp = c.take<uint32_t>(np + 1);
+  uint32_t* part_n = c.take<uint32_t>(np + 1);   // entries per part (nblk <= np)
   int32_t* perm = c.take<int32_t>(n_targets > 0 ? n_targets : 1);
   DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "tiles workspace carve failed");
   const int lpb = tile_lpb(tile_w);
   const int64_t nblk = (n_targets + lpb - 1) / lpb;
+  const int S = tile_sub();
+  DPS_REQUIRE(nblk * S < INT32_MAX, DPS_ERR_OVERFLOW, "too many tile-build blocks");
   const bool p16 = shift <= kP16MaxShift;   // counts and offsets are in entries
   const uint32_t per16 = p16 ? 8u : 4u;
   if (blk && t_rank && n_targets > 0) {
@@ -573,11 +777,19 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   if (blk) {
     DPS_HIP_RET(hipMemsetAsync(cntp, 0, (np + 1) * sizeof(uint32_t), st));
     DPS_HIP_RET(hipMemsetAsync(mxp, 0, (np + 1) * sizeof(uint32_t), st));
+    DPS_HIP_RET(hipMemsetAsync(curp, 0, (np + 1) * sizeof(uint32_t), st));
+    DPS_HIP_RET(hipMemsetAsync(part_n, 0, (nblk + 1) * sizeof(uint32_t), st));
+    if (n_targets > 0) {
+      k_part_entries<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(c_ptr, perm_or_null, n_targets,
+                                                                     lpb, part_n);
+      DPS_LAUNCHED();
+    }
     if (tile_maxc) DPS_HIP_RET(hipMemsetAsync(tile_maxc + nb, 0, sizeof(uint32_t), st));
     if (n_targets > 0 && nb > 0) {
-      k_tile_count_blk<<<static_cast<unsigned>(nblk), kBlkThreads, 0, st>>>(
+      k_tile_count_blk<<<static_cast<unsigned>(nblk * S), kBlkThreads, 0, st>>>(
           c_ptr, c_col, c_val, perm_or_null, tile_gmin ? g : nullptr, n_targets, n_mids, shift, T,
-          lpb, P, cntp, mxp, reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
+          lpb, P, S, part_n, cntp, mxp, reinterpret_cast<unsigned long long*>(tile_gmin),
+          status_dev);
       DPS_LAUNCHED();
     }
     if (nb > 0) {
@@ -589,8 +801,9 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, P, nb, p16 ? 1 : 0, tile_off);
     DPS_LAUNCHED();
     if (n_targets > 0 && nb > 0) {
-      k_tile_scatter_blk<<<static_cast<unsigned>(nblk), kBlkThreads, 0, st>>>(
-          c_ptr, c_col, c_val, perm_or_null, n_targets, n_mids, shift, T, lpb, P, off64, tile_ent);
+      k_tile_scatter_blk<<<static_cast<unsigned>(nblk * S), kBlkThreads, 0, st>>>(
+          c_ptr, c_col, c_val, perm_or_null, n_targets, n_mids, shift, T, lpb, P, S, part_n, off64,
+          curp, tile_ent);
       DPS_LAUNCHED();
     }
     if (nb > 0) {
