@@ -3,6 +3,8 @@
 // vectors s, g.  SURVEY.md §8a rows A2-A4.
 #include "dps_common.hpp"
 
+#include <cstdlib>
+
 namespace dps {
 namespace {
 
@@ -116,6 +118,173 @@ __global__ __launch_bounds__(kBlock) void k_scatter_rows(
     const int32_t r = rows[i];
     tmp[seg_ptr[r] + atomicAdd(&cursor[r], 1u)] = cols[i];
   }
+}
+
+// Two-level counting sort by row without global atomics (the per-pair global
+// atomics of k_count_rows / k_scatter_rows run at the fabric's atomic rate,
+// ~150-190 us per 7.5 M pairs on MI355X).  Level 1 buckets the pairs by row
+// range (2^rb rows per bucket) with LDS histograms per block of kL1Chunk pairs,
+// one exclusive scan over the [bucket][block] counts, and LDS cursors; level 2
+// is one workgroup per bucket: an LDS histogram of its rows, a block scan that
+// writes the bucket's seg_ptr entries directly (bucket start + local prefix),
+// and an LDS-cursor scatter of the columns into their row segments.  The order
+// inside a row segment is unspecified (seg_unique sorts it).
+constexpr int kL1Chunk = 4096;        // pairs per level-1 block (kBlock threads x 16)
+constexpr int kMaxBuckets = 4096;
+constexpr int kMaxRbShift = 12;       // rows per bucket <= 4096 (level-2 LDS histogram)
+
+__global__ __launch_bounds__(kBlock) void k_bucket_hist(const int32_t* __restrict__ rows,
+                                                        int64_t cap, const int64_t* n_dev,
+                                                        int rb, int n_buckets, int64_t n_blocks,
+                                                        uint32_t* __restrict__ H) {
+  __shared__ uint32_t h[kMaxBuckets];
+  for (int b = threadIdx.x; b < n_buckets; b += kBlock) h[b] = 0;
+  __syncthreads();
+  const int64_t n = bound_from(n_dev, cap);
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kL1Chunk;
+  const int64_t i1 = min(i0 + kL1Chunk, n);
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) atomicAdd(&h[rows[i] >> rb], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < n_buckets; b += kBlock)
+    H[static_cast<int64_t>(b) * n_blocks + blockIdx.x] = h[b];
+}
+
+// The block's pairs are first ordered by bucket in LDS (local counting sort),
+// then written out run by run, so consecutive threads write consecutive
+// addresses of a bucket's range instead of ~4 scattered pairs per bucket.
+__global__ __launch_bounds__(kBlock) void k_bucket_scatter(
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ cols, int64_t cap,
+    const int64_t* n_dev, int rb, int n_buckets, int64_t n_blocks,
+    const int64_t* __restrict__ Hoff, int32_t* __restrict__ trow, int32_t* __restrict__ tcol) {
+  __shared__ uint32_t cur[kMaxBuckets];     // local exclusive offsets, then cursors
+  __shared__ uint32_t loc0[kMaxBuckets];    // local exclusive offsets (kept)
+  __shared__ int32_t srow[kL1Chunk], scol[kL1Chunk];
+  __shared__ uint32_t wsum[kWavesPerBlock];
+  const int64_t n = bound_from(n_dev, cap);
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kL1Chunk;
+  const int64_t i1 = min(i0 + kL1Chunk, n);
+  if (i0 >= i1) return;   // block-uniform
+  const int m = static_cast<int>(i1 - i0);
+  for (int b = threadIdx.x; b < n_buckets; b += kBlock) cur[b] = 0;
+  __syncthreads();
+  constexpr int kPer = kL1Chunk / kBlock;
+  int32_t r[kPer], c[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int i = threadIdx.x + q * kBlock;
+    r[q] = i < m ? rows[i0 + i] : -1;
+    c[q] = i < m ? cols[i0 + i] : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (r[q] >= 0) atomicAdd(&cur[r[q] >> rb], 1u);
+  __syncthreads();
+  // exclusive scan of the local histogram (thread t: buckets [t*kq, (t+1)*kq))
+  constexpr int kq = kMaxBuckets / kBlock;
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  uint32_t h[kq], sum = 0;
+#pragma unroll
+  for (int q = 0; q < kq; ++q) {
+    const int b = threadIdx.x * kq + q;
+    h[q] = b < n_buckets ? cur[b] : 0u;
+    sum += h[q];
+  }
+  const uint32_t inc = wave_inclusive_sum(sum);
+  if (lane == kWave - 1) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+  for (int q = 0; q < kq; ++q) {
+    const int b = threadIdx.x * kq + q;
+    if (b < n_buckets) { cur[b] = run; loc0[b] = run; }
+    run += h[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    if (r[q] < 0) continue;
+    const uint32_t pos = atomicAdd(&cur[r[q] >> rb], 1u);
+    srow[pos] = r[q];
+    scol[pos] = c[q];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < m; i += kBlock) {
+    const int32_t rr = srow[i];
+    const int b = rr >> rb;
+    const int64_t o = Hoff[static_cast<int64_t>(b) * n_blocks + blockIdx.x] + (i - loc0[b]);
+    trow[o] = rr;
+    tcol[o] = scol[i];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_bucket_rows(
+    const int32_t* __restrict__ trow, const int32_t* __restrict__ tcol, int rb, int64_t n_rows,
+    int64_t n_blocks, const int64_t* __restrict__ Hoff, int64_t* __restrict__ seg_ptr,
+    int32_t* __restrict__ seg) {
+  __shared__ uint32_t cnt[1 << kMaxRbShift];
+  __shared__ uint32_t wsum[kWavesPerBlock];
+  const int64_t b = blockIdx.x;
+  const int64_t r0 = b << rb;
+  const int nr = static_cast<int>(min(static_cast<int64_t>(1) << rb, n_rows - r0));
+  const int64_t s = Hoff[b * n_blocks], e = Hoff[(b + 1) * n_blocks];
+  for (int r = threadIdx.x; r < nr; r += kBlock) cnt[r] = 0;
+  __syncthreads();
+  for (int64_t i = s + threadIdx.x; i < e; i += kBlock)
+    atomicAdd(&cnt[trow[i] - r0], 1u);
+  __syncthreads();
+  // exclusive scan of cnt[0..nr): thread t owns the run [t*per, (t+1)*per)
+  constexpr int kPer = (1 << kMaxRbShift) / kBlock;
+  const int lane = lane_id(), wave = threadIdx.x / kWave;
+  const int q0 = threadIdx.x * kPer;
+  uint32_t loc[kPer], sum = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    loc[q] = q0 + q < nr ? cnt[q0 + q] : 0u;
+    sum += loc[q];
+  }
+  const uint32_t inc = wave_inclusive_sum(sum);
+  if (lane == kWave - 1) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    if (q0 + q < nr) {
+      cnt[q0 + q] = run;
+      seg_ptr[r0 + q0 + q] = s + run;
+    }
+    run += loc[q];
+  }
+  if (r0 + nr == n_rows && threadIdx.x == 0) seg_ptr[n_rows] = e;
+  __syncthreads();
+  for (int64_t i = s + threadIdx.x; i < e; i += kBlock) {
+    const uint32_t pos = atomicAdd(&cnt[trow[i] - r0], 1u);
+    seg[s + pos] = tcol[i];
+  }
+}
+
+// Level-1 geometry for n_rows rows and at most cap pairs: about 8192 pairs per
+// bucket, at most kMaxBuckets buckets (ok = false: use the atomic path).
+struct BucketPlan {
+  bool ok;
+  int rb;
+  int n_buckets;
+  int64_t n_blocks;
+};
+BucketPlan bucket_plan(int64_t cap, int64_t n_rows) {
+  BucketPlan P{false, 0, 0, 0};
+  if (cap <= 0 || n_rows <= 0) return P;
+  int rb = 0;
+  while (rb < kMaxRbShift && (static_cast<double>(cap) * (1ll << (rb + 1))) / n_rows <= 8192.0) ++rb;
+  while (rb < kMaxRbShift && ((n_rows + (1ll << rb) - 1) >> rb) > kMaxBuckets) ++rb;
+  const int64_t nbk = (n_rows + (1ll << rb) - 1) >> rb;
+  if (nbk > kMaxBuckets) return P;
+  P.ok = true;
+  P.rb = rb;
+  P.n_buckets = static_cast<int>(nbk);
+  P.n_blocks = (cap + kL1Chunk - 1) / kL1Chunk;
+  return P;
 }
 
 // ---------------------------------------------------------------------------
@@ -741,6 +910,14 @@ size_t dps_csr_build_workspace_size(int64_t n_pairs, int64_t n_rows) {
   const size_t nr = static_cast<size_t>(n_rows > 0 ? n_rows : 1);
   const size_t np = static_cast<size_t>(n_pairs > 0 ? n_pairs : 1);
   size_t s = 0;
+  const BucketPlan B = bucket_plan(n_pairs, n_rows);
+  if (B.ok) {
+    const size_t nh = static_cast<size_t>(B.n_buckets) * static_cast<size_t>(B.n_blocks);
+    s += align_up((nh + 1) * sizeof(uint32_t));   // H
+    s += align_up((nh + 1) * sizeof(int64_t));    // Hoff
+    s += align_up(scan_workspace_size(static_cast<int64_t>(nh)));
+    s += 2 * align_up(np * sizeof(int32_t));      // bucketed rows, cols
+  }
   s += align_up(nr * sizeof(uint32_t));           // cnt
   s += align_up(nr * sizeof(uint32_t));           // cursor
   s += align_up((nr + 1) * sizeof(int64_t));      // seg_ptr
@@ -777,18 +954,42 @@ int dps_csr_build(const int32_t* rows, const int32_t* cols, int64_t n_pairs,
   void* gws = c.take<char>(seg_ws);
   DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "csr_build workspace carve failed");
 
-  DPS_HIP_RET(hipMemsetAsync(cnt, 0, nr * sizeof(uint32_t), st));
-  DPS_HIP_RET(hipMemsetAsync(cursor, 0, nr * sizeof(uint32_t), st));
-  if (n_pairs > 0) {
+  const BucketPlan B = bucket_plan(n_pairs, n_rows);
+  const char* env = std::getenv("DPATHSIM_CSR_ATOMIC");   // A/B: the per-pair atomic path
+  if (B.ok && !(env && std::atoi(env) != 0)) {
     DPS_REQUIRE(rows && cols, DPS_ERR_INVALID, "null input pairs");
-    k_count_rows<<<grid_for(n_pairs, kBlock), kBlock, 0, st>>>(rows, n_pairs, n_pairs_dev, cnt);
+    const int64_t nh = static_cast<int64_t>(B.n_buckets) * B.n_blocks;
+    uint32_t* H = c.take<uint32_t>(nh + 1);
+    int64_t* Hoff = c.take<int64_t>(nh + 1);
+    const size_t hs_ws = scan_workspace_size(nh);
+    void* hws = c.take<char>(hs_ws);
+    int32_t* trow = c.take<int32_t>(n_pairs);
+    int32_t* tcol = c.take<int32_t>(n_pairs);
+    DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "csr_build workspace carve failed");
+    k_bucket_hist<<<static_cast<unsigned>(B.n_blocks), kBlock, 0, st>>>(
+        rows, n_pairs, n_pairs_dev, B.rb, B.n_buckets, B.n_blocks, H);
     DPS_LAUNCHED();
-  }
-  DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, seg_ptr, n_rows, sws, scan_ws, st));
-  if (n_pairs > 0) {
-    k_scatter_rows<<<grid_for(n_pairs, kBlock), kBlock, 0, st>>>(rows, cols, n_pairs, n_pairs_dev,
-                                                                 seg_ptr, cursor, tmp);
+    DPS_HIP_RET(scan_exclusive<uint32_t>(H, Hoff, nh, hws, hs_ws, st));
+    k_bucket_scatter<<<static_cast<unsigned>(B.n_blocks), kBlock, 0, st>>>(
+        rows, cols, n_pairs, n_pairs_dev, B.rb, B.n_buckets, B.n_blocks, Hoff, trow, tcol);
     DPS_LAUNCHED();
+    k_bucket_rows<<<static_cast<unsigned>(B.n_buckets), kBlock, 0, st>>>(
+        trow, tcol, B.rb, n_rows, B.n_blocks, Hoff, seg_ptr, tmp);
+    DPS_LAUNCHED();
+  } else {
+    DPS_HIP_RET(hipMemsetAsync(cnt, 0, nr * sizeof(uint32_t), st));
+    DPS_HIP_RET(hipMemsetAsync(cursor, 0, nr * sizeof(uint32_t), st));
+    if (n_pairs > 0) {
+      DPS_REQUIRE(rows && cols, DPS_ERR_INVALID, "null input pairs");
+      k_count_rows<<<grid_for(n_pairs, kBlock), kBlock, 0, st>>>(rows, n_pairs, n_pairs_dev, cnt);
+      DPS_LAUNCHED();
+    }
+    DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, seg_ptr, n_rows, sws, scan_ws, st));
+    if (n_pairs > 0) {
+      k_scatter_rows<<<grid_for(n_pairs, kBlock), kBlock, 0, st>>>(rows, cols, n_pairs, n_pairs_dev,
+                                                                   seg_ptr, cursor, tmp);
+      DPS_LAUNCHED();
+    }
   }
   DPS_HIP_RET(seg_unique(tmp, nullptr, seg_ptr, n_rows, uniq, gws, seg_ws, st));
   DPS_HIP_RET(scan_exclusive<int64_t>(uniq, row_ptr, n_rows, sws, scan_ws, st));
