@@ -342,6 +342,9 @@ constexpr int kSel = 8;
 
 __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __restrict__ ent,
                                        int lane, Batch& B) {
+#ifdef DPS_PRIO_ISSUE
+  __builtin_amdgcn_s_setprio(DPS_PRIO_ISSUE);   // experiment: loads out first
+#endif
   const bool vl = lane < S.G.nv;
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
@@ -375,6 +378,9 @@ __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __
     B.e[u] = *reinterpret_cast<const uint4*>(ent + (live ? bj + 4u * static_cast<uint32_t>(q) : 0u));
     B.c[u] = live ? cj : 0;
   }
+#ifdef DPS_PRIO_ISSUE
+  __builtin_amdgcn_s_setprio(0);
+#endif
 }
 
 // Venues 64.. of a row with more than 64 venues: their buckets of tile t,

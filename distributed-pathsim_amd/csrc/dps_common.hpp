@@ -153,7 +153,8 @@ hipError_t scan_exclusive(const T* in, int64_t* out, int64_t n, void* ws, size_t
 // `counts` is non-null counts[seg_ptr[s] + i] = multiplicity of value i.
 size_t seg_unique_workspace_size(int64_t n_seg);
 hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, int64_t n_seg,
-                      int64_t* uniq, void* ws, size_t ws_bytes, hipStream_t stream);
+                      int64_t* uniq, void* ws, size_t ws_bytes, hipStream_t stream,
+                      int key_range = 0);
 
 // ---- stable LSD radix sort of (u64 key, u32 value) pairs (dps_sort.hip) ------
 // Sorts by the low key_bits bits of the keys; vals_in == nullptr means values

@@ -423,6 +423,8 @@ __device__ void block_bitonic_sort(int32_t* a, int len) {
   }
 }
 
+// Block-wide exclusive scan of one int per thread (NW waves per block).
+template <int NW>
 __device__ int64_t block_excl_scan_int(int v, int64_t* lds_w, int64_t* total) {
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
@@ -430,25 +432,32 @@ __device__ int64_t block_excl_scan_int(int v, int64_t* lds_w, int64_t* total) {
   if (lane == kWave - 1) lds_w[wave] = inc;
   __syncthreads();
   int64_t off = 0, tot = 0;
-  for (int w = 0; w < kWavesPerBlock; ++w) {
-    if (w < wave) off += lds_w[w];
-    tot += lds_w[w];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int64_t x = lds_w[w];
+    off += w < wave ? x : 0;
+    tot += x;
   }
   __syncthreads();
   *total = tot;
   return off + inc - v;
 }
 
-// Long segments: one block each; staged in LDS when they fit, else sorted in
-// place in global memory.  Then unique (+ run lengths) in 256-element chunks.
-__global__ __launch_bounds__(kBlock) void k_seg_long(int32_t* __restrict__ data,
-                                                     int32_t* __restrict__ counts,
-                                                     const int64_t* __restrict__ seg_ptr,
-                                                     int64_t* __restrict__ uniq,
-                                                     const int32_t* __restrict__ long_list,
-                                                     const unsigned* __restrict__ n_long) {
+// Long segments: one 1024-thread block each; staged in LDS when they fit, else
+// sorted in place in global memory.  Then unique (+ run lengths) in
+// block-sized chunks.
+constexpr int kLongBlock = 1024;
+constexpr int kRankSortMax = kLongBlock;   // segments up to this long: rank sort
+
+__global__ __launch_bounds__(kLongBlock) void k_seg_long(int32_t* __restrict__ data,
+                                                         int32_t* __restrict__ counts,
+                                                         const int64_t* __restrict__ seg_ptr,
+                                                         int64_t* __restrict__ uniq,
+                                                         const int32_t* __restrict__ long_list,
+                                                         const unsigned* __restrict__ n_long) {
   extern __shared__ __attribute__((aligned(16))) int32_t lds_seg[];
-  __shared__ int64_t lds_w[kWavesPerBlock];
+  constexpr int kNW = kLongBlock / kWave;
+  __shared__ int64_t lds_w[kNW];
   __shared__ int32_t lds_prev;
   const unsigned nl = *n_long;
   for (unsigned li = blockIdx.x; li < nl; li += gridDim.x) {
@@ -456,16 +465,36 @@ __global__ __launch_bounds__(kBlock) void k_seg_long(int32_t* __restrict__ data,
     const int64_t beg = seg_ptr[s];
     const int len = static_cast<int>(seg_ptr[s + 1] - beg);
     int32_t* a;
-    if (len <= kSegLdsCap) {
-      for (int i = threadIdx.x; i < len; i += kBlock) lds_seg[i] = data[beg + i];
+    if (len <= kRankSortMax) {
+      // rank sort (no barrier per phase): element i goes to the number of
+      // elements before it in (value, index) order; 4 values per LDS read
+      const int i = threadIdx.x;
+      const int32_t x = i < len ? data[beg + i] : INT_MAX;
+      const int len4 = (len + 3) & ~3;
+      lds_seg[i] = x;                              // padding: INT_MAX at index >= len
+      __syncthreads();
+      int r = 0;
+      for (int j = 0; j < len4; j += 4) {
+        const int4 v = *reinterpret_cast<const int4*>(lds_seg + j);
+        r += (v.x < x || (v.x == x && j < i)) ? 1 : 0;
+        r += (v.y < x || (v.y == x && j + 1 < i)) ? 1 : 0;
+        r += (v.z < x || (v.z == x && j + 2 < i)) ? 1 : 0;
+        r += (v.w < x || (v.w == x && j + 3 < i)) ? 1 : 0;
+      }
+      if (i < len) lds_seg[kRankSortMax + r] = x;  // padding ranks are never below len
+      __syncthreads();
+      a = lds_seg + kRankSortMax;
+    } else if (len <= kSegLdsCap) {
+      for (int i = threadIdx.x; i < len; i += kLongBlock) lds_seg[i] = data[beg + i];
       __syncthreads();
       a = lds_seg;
+      block_bitonic_sort(a, len);
     } else {
       a = data + beg;
+      block_bitonic_sort(a, len);
     }
-    block_bitonic_sort(a, len);
     int64_t carry = 0;
-    for (int c0 = 0; c0 < len; c0 += kBlock) {
+    for (int c0 = 0; c0 < len; c0 += kLongBlock) {
       const int i = c0 + threadIdx.x;
       const bool valid = i < len;
       const int32_t v = valid ? a[i] : 0;
@@ -473,9 +502,9 @@ __global__ __launch_bounds__(kBlock) void k_seg_long(int32_t* __restrict__ data,
       if (valid && i > 0) prev = (threadIdx.x == 0) ? lds_prev : a[i - 1];
       const bool first = valid && (i == 0 || v != prev);
       __syncthreads();  // every read of this chunk happens before any write below
-      if (threadIdx.x == kBlock - 1 || i == len - 1) lds_prev = v;
+      if (threadIdx.x == kLongBlock - 1 || i == len - 1) lds_prev = v;
       int64_t tot;
-      const int64_t rank = carry + block_excl_scan_int(first ? 1 : 0, lds_w, &tot);
+      const int64_t rank = carry + block_excl_scan_int<kNW>(first ? 1 : 0, lds_w, &tot);
       if (first) {
         data[beg + rank] = v;
         if (counts) counts[beg + rank] = i;  // position for now; turned into lengths below
@@ -484,7 +513,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_long(int32_t* __restrict__ data,
       __syncthreads();
     }
     if (counts) {
-      for (int64_t u0 = 0; u0 < carry; u0 += kBlock) {
+      for (int64_t u0 = 0; u0 < carry; u0 += kLongBlock) {
         const int64_t u = u0 + threadIdx.x;
         int32_t here = 0, next = 0;
         if (u < carry) {
@@ -497,6 +526,54 @@ __global__ __launch_bounds__(kBlock) void k_seg_long(int32_t* __restrict__ data,
       }
     }
     if (threadIdx.x == 0) uniq[s] = carry;
+    __syncthreads();
+  }
+}
+
+// Long segments over a small key range (values < key_range <= kHistKeys, or
+// INT_MAX = "none", which sorts last): an LDS histogram per segment replaces
+// the sort -- the nonzero bins in order ARE the sorted distinct values and
+// their run lengths (the single-mid SpGEMM's venue rows).
+constexpr int kHistKeys = 8192;
+
+__global__ __launch_bounds__(kBlock) void k_seg_long_hist(int32_t* __restrict__ data,
+                                                          int32_t* __restrict__ counts,
+                                                          const int64_t* __restrict__ seg_ptr,
+                                                          int64_t* __restrict__ uniq,
+                                                          const int32_t* __restrict__ long_list,
+                                                          const unsigned* __restrict__ n_long,
+                                                          int key_range) {
+  __shared__ uint32_t hist[kHistKeys + 1];
+  __shared__ int64_t lds_w[kWavesPerBlock];
+  const int nb = key_range + 1;                      // bin key_range: INT_MAX
+  const int per = (nb + kBlock - 1) / kBlock;        // bins per thread (contiguous)
+  const unsigned nl = *n_long;
+  for (unsigned li = blockIdx.x; li < nl; li += gridDim.x) {
+    const int64_t s = long_list[li];
+    const int64_t beg = seg_ptr[s];
+    const int len = static_cast<int>(seg_ptr[s + 1] - beg);
+    for (int b = threadIdx.x; b < nb; b += kBlock) hist[b] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < len; i += kBlock) {
+      const int32_t v = data[beg + i];
+      atomicAdd(&hist[v < key_range ? v : key_range], 1u);
+    }
+    __syncthreads();
+    const int b0 = threadIdx.x * per;
+    int nz = 0;
+    for (int q = 0; q < per; ++q) nz += (b0 + q < nb && hist[b0 + q] != 0) ? 1 : 0;
+    int64_t tot;
+    int64_t rank = block_excl_scan_int<kWavesPerBlock>(nz, lds_w, &tot);
+    for (int q = 0; q < per; ++q) {
+      const int b = b0 + q;
+      if (b >= nb) break;
+      const uint32_t h = hist[b];
+      if (!h) continue;
+      data[beg + rank] = b < key_range ? b : INT_MAX;
+      if (counts) counts[beg + rank] = static_cast<int32_t>(h);
+      ++rank;
+    }
+    if (threadIdx.x == 0) uniq[s] = tot;
     __syncthreads();
   }
 }
@@ -861,7 +938,8 @@ size_t seg_unique_workspace_size(int64_t n_seg) {
 }
 
 hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, int64_t n_seg,
-                      int64_t* uniq, void* ws, size_t ws_bytes, hipStream_t stream) {
+                      int64_t* uniq, void* ws, size_t ws_bytes, hipStream_t stream,
+                      int key_range) {
   Carve c(ws, ws_bytes);
   int32_t* long_list = c.take<int32_t>(n_seg > 0 ? n_seg : 1);
   unsigned* n_long = c.take<unsigned>(1);
@@ -873,8 +951,13 @@ hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, in
                                                                       n_seg, uniq, long_list,
                                                                       n_long);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  k_seg_long<<<512, kBlock, kSegLdsCap * sizeof(int32_t), stream>>>(data, counts, seg_ptr, uniq,
-                                                                   long_list, n_long);
+  if (key_range > 0 && key_range <= kHistKeys) {
+    k_seg_long_hist<<<1024, kBlock, 0, stream>>>(data, counts, seg_ptr, uniq, long_list, n_long,
+                                                 key_range);
+    return hipGetLastError();
+  }
+  k_seg_long<<<512, kLongBlock, kSegLdsCap * sizeof(int32_t), stream>>>(data, counts, seg_ptr,
+                                                                       uniq, long_list, n_long);
   return hipGetLastError();
 }
 

@@ -507,14 +507,14 @@ size_t dps_spgemm_single_workspace_size(int64_t n_out_rows, int64_t nnz_ap, int6
 
 int dps_spgemm_single(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_out_rows,
                       int64_t nnz_ap_cap, const int64_t* px_ptr, const int32_t* px_col,
-                      int64_t n_papers, int64_t* c_ptr, int32_t* c_col, int32_t* c_val,
-                      int64_t* c_nnz, void* ws, size_t ws_bytes, void* stream) {
+                      int64_t n_papers, int64_t n_mids, int64_t* c_ptr, int32_t* c_col,
+                      int32_t* c_val, int64_t* c_nnz, void* ws, size_t ws_bytes, void* stream) {
   DPS_REQUIRE(n_out_rows >= 0 && nnz_ap_cap >= 0, DPS_ERR_INVALID, "negative size");
   DPS_REQUIRE(c_ptr && c_nnz, DPS_ERR_INVALID, "null output");
   DPS_REQUIRE(!c_col == !c_val, DPS_ERR_INVALID, "c_col and c_val must both be set (numeric)");
   DPS_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 256 == 0, DPS_ERR_WORKSPACE,
               "workspace not 256-byte aligned");
-  DPS_REQUIRE(n_papers >= 0, DPS_ERR_INVALID, "negative n_papers");
+  DPS_REQUIRE(n_papers >= 0 && n_mids >= 0, DPS_ERR_INVALID, "negative n_papers / n_mids");
   DPS_REQUIRE(ws_bytes >= dps_spgemm_single_workspace_size(n_out_rows, nnz_ap_cap, n_papers),
               DPS_ERR_WORKSPACE, "spgemm_single workspace too small");
   auto st = static_cast<hipStream_t>(stream);
@@ -538,7 +538,8 @@ int dps_spgemm_single(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_ou
       k_mid_of_entry<<<grid_for(nnz_ap_cap, kBlock), kBlock, 0, st>>>(ap_ptr, ap_col, n_out_rows,
                                                                      vp, mids);
       DPS_LAUNCHED();
-      DPS_HIP_RET(seg_unique(mids, cnt, ap_ptr, n_out_rows, uniq, gws, seg_ws, st));
+      DPS_HIP_RET(seg_unique(mids, cnt, ap_ptr, n_out_rows, uniq, gws, seg_ws, st,
+                             n_mids < INT32_MAX ? static_cast<int>(n_mids) : 0));
       k_drop_none<<<grid_for(n_out_rows, kBlock), kBlock, 0, st>>>(mids, ap_ptr, n_out_rows, uniq);
       DPS_LAUNCHED();
     }

@@ -35,6 +35,23 @@ def max_shard(n_rows: int, world: int, bounds=None) -> int:
     return max(b - a for a, b in bounds)
 
 
+def balanced_edges(work: torch.Tensor, world: int) -> torch.Tensor:
+    """Shard edges [0, e_1, ..., n] (int64 tensor on work's device, nothing read
+    back): rank r gets the rows whose work prefix falls in [r/world,
+    (r+1)/world) of the total.  See :func:`balanced_bounds`."""
+    n = int(work.numel())
+    if world < 1:
+        raise ValueError(f"bad world {world}")
+    if world == 1 or n == 0:
+        return torch.tensor([shard_bounds(n, r, world)[0] for r in range(world)] + [n],
+                            dtype=torch.int64, device=work.device)
+    pre = torch.cumsum(work.to(torch.int64), 0)
+    cuts = torch.arange(1, world, device=pre.device, dtype=torch.int64) * pre[-1] // world
+    idx = torch.searchsorted(pre, cuts, right=True).clamp_(0, n)
+    edges = torch.cat([idx.new_zeros(1), idx, idx.new_full((1,), n)])
+    return torch.cummax(edges, 0).values
+
+
 def balanced_bounds(work: torch.Tensor, world: int) -> list[tuple[int, int]]:
     """Contiguous shards of (nearly) equal total work.
 
@@ -43,18 +60,7 @@ def balanced_bounds(work: torch.Tensor, world: int) -> list[tuple[int, int]]:
     [r/world, (r+1)/world) of the total.  Every rank computes the same bounds
     from the same C, so no communication is needed.
     """
-    n = int(work.numel())
-    if world < 1:
-        raise ValueError(f"bad world {world}")
-    if world == 1 or n == 0:
-        return [shard_bounds(n, r, world) for r in range(world)]
-    pre = torch.cumsum(work.to(torch.int64), 0)
-    total = pre[-1]
-    cuts = torch.arange(1, world, device=pre.device, dtype=torch.int64) * total // world
-    idx = torch.searchsorted(pre, cuts, right=True).cpu().tolist()
-    edges = [0] + [min(max(int(i), 0), n) for i in idx] + [n]
-    for i in range(1, len(edges)):
-        edges[i] = max(edges[i], edges[i - 1])
+    edges = balanced_edges(work, world).cpu().tolist()
     return [(edges[r], edges[r + 1]) for r in range(world)]
 
 

@@ -136,6 +136,7 @@ class PathSimEngine:
         st = self.stream
         bnd = self.bounds
         N, E = t.graph.n_nodes, t.graph.n_edges
+        NR = t.n_rows             # C row space: authors, other AP sources, one empty row
         NA, NP, NV = t.n_authors, t.n_papers, t.n_mids
         info = self.info = BuildInfo(n_nodes=N, n_edges=E, n_authors=NA, n_papers=NP, n_mids=NV)
         self.checked = False
@@ -160,12 +161,12 @@ class PathSimEngine:
                       _ptr(px_r), _ptr(px_c), _ptr(n_px), st)
             mark("extract")
             # A2/A3: typed CSR build (distinct)
-            ws_bytes = max(_lib.size("dps_csr_build_workspace_size", E, N),
+            ws_bytes = max(_lib.size("dps_csr_build_workspace_size", E, NR),
                            _lib.size("dps_csr_build_workspace_size", E, NP))
             ws = self._ws(ws_bytes)
-            ap_ptr, ap_col = self._empty(N + 1, torch.int64), self._empty(E, torch.int32)
+            ap_ptr, ap_col = self._empty(NR + 1, torch.int64), self._empty(E, torch.int32)
             ap_nnz = self._empty(1, torch.int64)
-            _lib.call("dps_csr_build", _ptr(ap_r), _ptr(ap_c), E, _ptr(n_ap), N, _ptr(ap_ptr),
+            _lib.call("dps_csr_build", _ptr(ap_r), _ptr(ap_c), E, _ptr(n_ap), NR, _ptr(ap_ptr),
                       _ptr(ap_col), _ptr(ap_nnz), _ptr(ws), ws.numel(), st)
             px_ptr, px_col = self._empty(NP + 1, torch.int64), self._empty(E, torch.int32)
             px_nnz = self._empty(1, torch.int64)
@@ -179,21 +180,21 @@ class PathSimEngine:
             # at most one mid (APVPA): gather + segmented unique; otherwise the
             # hash SpGEMM.
             cap = bnd.sum_c
-            c_ptr, c_nnz = self._empty(N + 1, torch.int64), self._empty(2, torch.int64)
+            c_ptr, c_nnz = self._empty(NR + 1, torch.int64), self._empty(2, torch.int64)
             sp_status = self._empty(1, torch.int32)
             c_col, c_val = self._empty(cap, torch.int32), self._empty(cap, torch.int32)
             if bnd.max_mids_per_paper <= 1:
-                sws = self._ws(_lib.size("dps_spgemm_single_workspace_size", N, E, NP))
+                sws = self._ws(_lib.size("dps_spgemm_single_workspace_size", NR, E, NP))
                 sp_status.zero_()
                 for numeric in (False, True):
-                    _lib.call("dps_spgemm_single", _ptr(ap_ptr), _ptr(ap_col), N, E, _ptr(px_ptr),
-                              _ptr(px_col), NP, _ptr(c_ptr), _ptr(c_col) if numeric else None,
+                    _lib.call("dps_spgemm_single", _ptr(ap_ptr), _ptr(ap_col), NR, E, _ptr(px_ptr),
+                              _ptr(px_col), NP, NV, _ptr(c_ptr), _ptr(c_col) if numeric else None,
                               _ptr(c_val) if numeric else None, _ptr(c_nnz), _ptr(sws),
                               sws.numel(), st)
             else:
-                sws = self._ws(_lib.size("dps_spgemm_hash_workspace_size", N, bnd.max_row_expand))
+                sws = self._ws(_lib.size("dps_spgemm_hash_workspace_size", NR, bnd.max_row_expand))
                 for numeric in (False, True):
-                    _lib.call("dps_spgemm_hash", _ptr(ap_ptr), _ptr(ap_col), None, N, _ptr(px_ptr),
+                    _lib.call("dps_spgemm_hash", _ptr(ap_ptr), _ptr(ap_col), None, NR, _ptr(px_ptr),
                               _ptr(px_col), bnd.max_row_expand, _ptr(c_ptr),
                               _ptr(c_col) if numeric else None, _ptr(c_val) if numeric else None,
                               _ptr(c_nnz), _ptr(sp_status), _ptr(sws), sws.numel(), st)
@@ -202,7 +203,7 @@ class PathSimEngine:
             # A4: s = column sums of C over ALL AP rows, g = C.s over author rows,
             # diag, stats
             s = self._empty(NV, torch.int64)
-            _lib.call("dps_col_sums", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), N, NV, _ptr(s), st)
+            _lib.call("dps_col_sums", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NR, NV, _ptr(s), st)
             g = self._empty(NA, torch.int64)
             diag = self._empty(NA, torch.int64)
             stats = self._empty(_lib.STATS_LEN, torch.int64)

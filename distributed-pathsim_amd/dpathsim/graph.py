@@ -160,10 +160,6 @@ class TypedTables:
         self.n_authors = int(is_author.sum())
         self.n_papers = int(is_paper.sum())
         self.n_mids = int(is_mid.sum())
-        rowid = np.empty(graph.n_nodes, dtype=np.int64)
-        rowid[is_author] = np.arange(self.n_authors)
-        rowid[~is_author] = self.n_authors + np.arange(graph.n_nodes - self.n_authors)
-        self.node_rowid = rowid.astype(np.int32)
         colid = np.full(graph.n_nodes, -1, dtype=np.int64)
         colid[is_paper] = np.arange(self.n_papers)
         colid[is_mid] = np.arange(self.n_mids)
@@ -177,6 +173,22 @@ class TypedTables:
         self.edge_rel = np.ascontiguousarray(
             rel_code[graph.edge_rel_idx] if graph.n_edges else np.zeros(0, np.uint8),
             dtype=np.uint8)
+        # C row space: authors [0, N_A) in node order, then the other sources
+        # of AP incidences (author_of edges into a paper; the source type is not
+        # checked, DPathSim_APVPA.py:78-84) in node order, then ONE shared empty
+        # row for every node that can have no C entries -- so the device build's
+        # row-indexed passes run over N_A + K + 1 rows, not over every node.
+        is_src = np.zeros(graph.n_nodes, dtype=bool)
+        if graph.n_edges:
+            ap = (self.edge_rel == _lib.R_AP) & is_paper[graph.edge_dst]
+            is_src[graph.edge_src[ap]] = True
+        other = is_src & ~is_author
+        n_other = int(other.sum())
+        rowid = np.full(graph.n_nodes, self.n_authors + n_other, dtype=np.int64)
+        rowid[is_author] = np.arange(self.n_authors)
+        rowid[other] = self.n_authors + np.arange(n_other)
+        self.node_rowid = rowid.astype(np.int32)
+        self.n_rows = self.n_authors + n_other + 1
         if graph.n_nodes >= 2 ** 31 - 1:
             raise OverflowError("more than 2^31-1 nodes")
 

@@ -154,15 +154,17 @@ int dps_spgemm_hash(const int64_t* ap_ptr, const int32_t* ap_col, const int32_t*
  * unique over the AP rows (a paper -> mid map of n_papers entries first makes
  * that gather one random read).  Output rows = AP rows [0, n_out_rows) (ap_ptr with
  * n_out_rows + 1 entries; the AP CSR must cover exactly these rows).
- * nnz_ap_cap >= ap_ptr[n_out_rows] sizes the workspace.  Same two phases as
- * dps_spgemm_hash.  A paper with two or more mids is a caller error (the
+ * nnz_ap_cap >= ap_ptr[n_out_rows] sizes the workspace.  n_mids: every
+ * px_col value is below it (rows longer than 64 are then reduced by an LDS
+ * histogram instead of a sort when n_mids <= 8192; 0 = unknown, always sort).
+ * Same two phases as dps_spgemm_hash.  A paper with two or more mids is a caller error (the
  * engine chooses this path only when the raw edges give no paper two). */
 size_t dps_spgemm_single_workspace_size(int64_t n_out_rows, int64_t nnz_ap_cap,
                                         int64_t n_papers);
 int dps_spgemm_single(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_out_rows,
                       int64_t nnz_ap_cap, const int64_t* px_ptr, const int32_t* px_col,
-                      int64_t n_papers, int64_t* c_ptr, int32_t* c_col, int32_t* c_val,
-                      int64_t* c_nnz, void* ws, size_t ws_bytes, void* stream);
+                      int64_t n_papers, int64_t n_mids, int64_t* c_ptr, int32_t* c_col,
+                      int32_t* c_val, int64_t* c_nnz, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * A4. Global walk ingredients.

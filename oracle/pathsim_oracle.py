@@ -255,7 +255,8 @@ class COracle:
               & (typed.node_type[g.edge_dst] == 3))
         return cls(typed.node_rowid[g.edge_src[ap]], typed.node_colid[g.edge_dst[ap]],
                    typed.node_colid[g.edge_src[px]], typed.node_colid[g.edge_dst[px]],
-                   g.n_nodes, typed.n_authors, typed.n_papers, typed.n_mids)
+                   getattr(typed, "n_rows", g.n_nodes), typed.n_authors, typed.n_papers,
+                   typed.n_mids)
 
     def export(self):
         nnz = self._lib.orc_nnz(self._st)

@@ -51,7 +51,15 @@ def test_typed_tables_dblp_small(dblp_small_tuples):
     assert (t.n_authors, t.n_papers, t.n_mids) == (770, 1001, 85)
     authors = [x[0] for x in v if x[2] == "author"]
     assert [g.node_id(int(i)) for i in t.author_nodes] == authors
-    assert sorted(t.node_rowid.tolist()) == list(range(g.n_nodes))
+    # C row space: authors first (node order), then the other AP sources, then
+    # one shared empty row for every other node
+    assert np.array_equal(t.node_rowid[t.author_nodes], np.arange(770))
+    ap = (t.edge_rel == _lib.R_AP) & (t.node_type[np.asarray(g.edge_dst)] == _lib.T_PAPER)
+    srcs = np.unique(np.asarray(g.edge_src)[ap])
+    assert len(np.unique(t.node_rowid[srcs])) == len(srcs)
+    rest = np.setdiff1d(np.arange(g.n_nodes), np.concatenate([srcs, t.author_nodes]))
+    assert (t.node_rowid[rest] == t.n_rows - 1).all()
+    assert t.n_rows == 770 + len(np.setdiff1d(srcs, t.author_nodes)) + 1
     assert int((t.edge_rel == _lib.R_AP).sum()) == 1265
     assert int((t.edge_rel == _lib.R_PX).sum()) == 1001
     assert g.vertices() == v and g.edges() == e
