@@ -454,13 +454,22 @@ __global__ __launch_bounds__(kLongBlock) void k_seg_long(int32_t* __restrict__ d
                                                          const int64_t* __restrict__ seg_ptr,
                                                          int64_t* __restrict__ uniq,
                                                          const int32_t* __restrict__ long_list,
-                                                         const unsigned* __restrict__ n_long) {
+                                                         const unsigned* __restrict__ n_long,
+                                                         unsigned* __restrict__ next) {
   extern __shared__ __attribute__((aligned(16))) int32_t lds_seg[];
   constexpr int kNW = kLongBlock / kWave;
   __shared__ int64_t lds_w[kNW];
   __shared__ int32_t lds_prev;
+  __shared__ unsigned li_s;
   const unsigned nl = *n_long;
-  for (unsigned li = blockIdx.x; li < nl; li += gridDim.x) {
+  // segments are taken from a queue (one atomic per segment): a block that
+  // drew a few long ones does not hold up the rest of the list
+  for (;;) {
+    if (threadIdx.x == 0) li_s = atomicAdd(next, 1u);
+    __syncthreads();
+    const unsigned li = li_s;
+    __syncthreads();
+    if (li >= nl) break;
     const int64_t s = long_list[li];
     const int64_t beg = seg_ptr[s];
     const int len = static_cast<int>(seg_ptr[s + 1] - beg);
@@ -548,6 +557,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_long_hist(int32_t* __restrict__ 
   const int nb = key_range + 1;                      // bin key_range: INT_MAX
   const int per = (nb + kBlock - 1) / kBlock;        // bins per thread (contiguous)
   const unsigned nl = *n_long;
+  // static assignment (a per-segment queue measured 2x slower here: the
+  // segments are short and uniform, the queue's two barriers are not)
   for (unsigned li = blockIdx.x; li < nl; li += gridDim.x) {
     const int64_t s = long_list[li];
     const int64_t beg = seg_ptr[s];
@@ -782,13 +793,18 @@ __global__ __launch_bounds__(kBlock) void k_global_walks(const int64_t* __restri
                                                          const int64_t* __restrict__ s,
                                                          int64_t* __restrict__ g,
                                                          int64_t* __restrict__ diag,
-                                                         unsigned long long* __restrict__ stats) {
+                                                         unsigned long long* __restrict__ stats,
+                                                         const unsigned* __restrict__ n_v,
+                                                         int64_t* __restrict__ terms) {
   // A wave owns 64 consecutive rows, whose entries are one contiguous range of
   // C: it walks that range in coalesced 64-entry strips (a lane finds its row
   // by a 6-step search over the row offsets) and sums per row in LDS, so a
-  // heavy row costs strips, not one lane's serial loop.
+  // heavy row costs strips, not one lane's serial loop.  (Measured slower: an
+  // LDS start-marker + DPP max-scan instead of the search, +6 %; a wave
+  // reduction for strips inside one row instead of its LDS atomics, +13 %.)
   __shared__ unsigned long long acc_g[kWavesPerBlock][kWave];
   __shared__ unsigned long long acc_d[kWavesPerBlock][kWave];
+  __shared__ unsigned long long acc_t[kWavesPerBlock][kWave];   // row work (n_v given)
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
   int64_t max_c = 0, max_d = 0, max_g = 0;
@@ -803,6 +819,7 @@ __global__ __launch_bounds__(kBlock) void k_global_walks(const int64_t* __restri
         c_ptr[r0 + kWave < n_rows ? r0 + kWave : n_rows] - base);
     acc_g[wave][lane] = 0;
     acc_d[wave][lane] = 0;
+    acc_t[wave][lane] = 0;
     __builtin_amdgcn_wave_barrier();
     for (uint32_t e0 = 0; e0 < total; e0 += kWave) {
       const uint32_t i = e0 + lane;
@@ -810,8 +827,10 @@ __global__ __launch_bounds__(kBlock) void k_global_walks(const int64_t* __restri
       if (i < total) {
         const int64_t j = base + i;
         const int64_t c = c_val[j];
-        atomicAdd(&acc_g[wave][o], static_cast<unsigned long long>(c * s[c_col[j]]));
+        const int32_t v = c_col[j];
+        atomicAdd(&acc_g[wave][o], static_cast<unsigned long long>(c * s[v]));
         atomicAdd(&acc_d[wave][o], static_cast<unsigned long long>(c * c));
+        if (n_v) atomicAdd(&acc_t[wave][o], static_cast<unsigned long long>(n_v[v]));
         max_c = c > max_c ? c : max_c;
       }
     }
@@ -823,6 +842,7 @@ __global__ __launch_bounds__(kBlock) void k_global_walks(const int64_t* __restri
       const int64_t dx = static_cast<int64_t>(acc_d[wave][lane]);
       g[x] = gx;
       if (diag) diag[x] = dx;
+      if (terms) terms[x] = static_cast<int64_t>(acc_t[wave][lane]);
       max_d = dx > max_d ? dx : max_d;
       max_g = gx > max_g ? gx : max_g;
     }
@@ -910,24 +930,34 @@ __global__ __launch_bounds__(kBlock) void k_col_sums(const int64_t* __restrict__
                                                      const int32_t* __restrict__ c_col,
                                                      const int32_t* __restrict__ c_val,
                                                      int64_t n_rows, int64_t n_mids,
-                                                     unsigned long long* __restrict__ s) {
+                                                     unsigned long long* __restrict__ s,
+                                                     int64_t n_count_rows,
+                                                     unsigned* __restrict__ n_v) {
   // block (x, y) sums the mids [y*kSumLds, (y+1)*kSumLds) of its share of the
-  // entries in LDS, one global atomic per mid and block
+  // entries in LDS, one global atomic per mid and block; with n_v it also
+  // counts the entries of rows [0, n_count_rows) per mid (the hot kernel's
+  // row-work weights: C^T holds the author rows only)
   __shared__ unsigned long long h[kSumLds];
+  __shared__ unsigned hc[kSumLds];
   const int64_t m0 = static_cast<int64_t>(blockIdx.y) * kSumLds;
   const int64_t m1 = min(m0 + kSumLds, n_mids);
-  for (int64_t i = threadIdx.x; i < m1 - m0; i += kBlock) h[i] = 0;
+  for (int64_t i = threadIdx.x; i < m1 - m0; i += kBlock) { h[i] = 0; hc[i] = 0; }
   __syncthreads();
   const int64_t b0 = c_ptr[0], nnz = c_ptr[n_rows] - b0;
+  const int64_t ncnt = n_v ? c_ptr[n_count_rows] - b0 : 0;
   for (int64_t j = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; j < nnz;
        j += static_cast<int64_t>(gridDim.x) * kBlock) {
     const int64_t v = c_col[b0 + j];
-    if (v >= m0 && v < m1)
+    if (v >= m0 && v < m1) {
       atomicAdd(&h[v - m0], static_cast<unsigned long long>(c_val[b0 + j]));
+      if (j < ncnt) atomicAdd(&hc[v - m0], 1u);
+    }
   }
   __syncthreads();
-  for (int64_t i = threadIdx.x; i < m1 - m0; i += kBlock)
+  for (int64_t i = threadIdx.x; i < m1 - m0; i += kBlock) {
     if (h[i]) atomicAdd(&s[m0 + i], h[i]);
+    if (n_v && hc[i]) atomicAdd(&n_v[m0 + i], hc[i]);
+  }
 }
 
 }  // namespace
@@ -942,9 +972,9 @@ hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, in
                       int key_range) {
   Carve c(ws, ws_bytes);
   int32_t* long_list = c.take<int32_t>(n_seg > 0 ? n_seg : 1);
-  unsigned* n_long = c.take<unsigned>(1);
+  unsigned* n_long = c.take<unsigned>(2);   // [0] list length, [1] queue head
   if (!c.ok) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(n_long, 0, sizeof(unsigned), stream);
+  hipError_t e = hipMemsetAsync(n_long, 0, 2 * sizeof(unsigned), stream);
   if (e != hipSuccess) return e;
   if (n_seg <= 0) return hipSuccess;
   k_seg_short<<<grid_for(n_seg, kBlock), kBlock, 0, stream>>>(data, counts, seg_ptr,
@@ -956,8 +986,8 @@ hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, in
                                                  key_range);
     return hipGetLastError();
   }
-  k_seg_long<<<512, kLongBlock, kSegLdsCap * sizeof(int32_t), stream>>>(data, counts, seg_ptr,
-                                                                       uniq, long_list, n_long);
+  k_seg_long<<<512, kLongBlock, kSegLdsCap * sizeof(int32_t), stream>>>(
+      data, counts, seg_ptr, uniq, long_list, n_long, n_long + 1);
   return hipGetLastError();
 }
 
@@ -1191,7 +1221,36 @@ int dps_global_walks(const int64_t* c_ptr, const int32_t* c_col, const int32_t* 
   auto st = static_cast<hipStream_t>(stream);
   if (stats) DPS_HIP_RET(hipMemsetAsync(stats, 0, DPS_STATS_LEN * sizeof(int64_t), st));
   k_global_walks<<<grid_for(n_rows, kBlock), kBlock, 0, st>>>(
-      c_ptr, c_col, c_val, n_rows, s, g, diag, reinterpret_cast<unsigned long long*>(stats));
+      c_ptr, c_col, c_val, n_rows, s, g, diag, reinterpret_cast<unsigned long long*>(stats),
+      nullptr, nullptr);
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
+int dps_walks_fused(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                    int64_t n_rows, int64_t n_authors, int64_t n_mids, int64_t* s,
+                    uint32_t* n_v, int64_t* g, int64_t* diag, int64_t* terms, int64_t* stats,
+                    void* stream) {
+  DPS_REQUIRE(n_rows >= 0 && n_authors >= 0 && n_authors <= n_rows && n_mids >= 0,
+              DPS_ERR_INVALID, "bad sizes");
+  DPS_REQUIRE(c_ptr && g && (n_mids == 0 || (s && n_v)), DPS_ERR_INVALID, "null array");
+  auto st = static_cast<hipStream_t>(stream);
+  if (stats) DPS_HIP_RET(hipMemsetAsync(stats, 0, DPS_STATS_LEN * sizeof(int64_t), st));
+  if (n_mids > 0) {
+    DPS_HIP_RET(hipMemsetAsync(s, 0, n_mids * sizeof(int64_t), st));
+    DPS_HIP_RET(hipMemsetAsync(n_v, 0, n_mids * sizeof(uint32_t), st));
+    if (n_rows > 0) {
+      const unsigned ny = static_cast<unsigned>((n_mids + kSumLds - 1) / kSumLds);
+      k_col_sums<<<dim3(ny > 1 ? 256 : 512, ny), kBlock, 0, st>>>(
+          c_ptr, c_col, c_val, n_rows, n_mids, reinterpret_cast<unsigned long long*>(s),
+          n_authors, n_v);
+      DPS_LAUNCHED();
+    }
+  }
+  if (n_authors == 0) return DPS_OK;
+  k_global_walks<<<grid_for(n_authors, kBlock), kBlock, 0, st>>>(
+      c_ptr, c_col, c_val, n_authors, s, g, diag, reinterpret_cast<unsigned long long*>(stats),
+      n_mids > 0 ? n_v : nullptr, terms);
   DPS_LAUNCHED();
   return DPS_OK;
 }
@@ -1206,7 +1265,7 @@ int dps_col_sums(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   if (n_rows == 0) return DPS_OK;
   const unsigned ny = static_cast<unsigned>((n_mids + kSumLds - 1) / kSumLds);
   k_col_sums<<<dim3(ny > 1 ? 256 : 512, ny), kBlock, 0, st>>>(
-      c_ptr, c_col, c_val, n_rows, n_mids, reinterpret_cast<unsigned long long*>(s));
+      c_ptr, c_col, c_val, n_rows, n_mids, reinterpret_cast<unsigned long long*>(s), 0, nullptr);
   DPS_LAUNCHED();
   return DPS_OK;
 }

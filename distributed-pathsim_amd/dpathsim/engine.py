@@ -202,13 +202,15 @@ class PathSimEngine:
             mark("spgemm")
             # A4: s = column sums of C over ALL AP rows, g = C.s over author rows,
             # diag, stats
+            # ... and, in the same two passes over C, the hot kernel's row work
             s = self._empty(NV, torch.int64)
-            _lib.call("dps_col_sums", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NR, NV, _ptr(s), st)
+            n_v = self._empty(NV, torch.int32)
             g = self._empty(NA, torch.int64)
             diag = self._empty(NA, torch.int64)
+            terms = self._empty(NA, torch.int64)
             stats = self._empty(_lib.STATS_LEN, torch.int64)
-            _lib.call("dps_global_walks", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NA, _ptr(s),
-                      _ptr(g), _ptr(diag), _ptr(stats), st)
+            _lib.call("dps_walks_fused", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NR, NA, NV,
+                      _ptr(s), _ptr(n_v), _ptr(g), _ptr(diag), _ptr(terms), _ptr(stats), st)
             mark("walks")
             # the per-author denominator term of the score
             den = g if self.denominator == "rowsum" else diag
@@ -238,7 +240,7 @@ class PathSimEngine:
             mark("tiles")
             del tws
         d.pop("row_work", None)
-        d.update(ap_ptr=ap_ptr, ap_col=ap_col, px_ptr=px_ptr, px_col=px_col, c_ptr=c_ptr,
+        d.update(row_terms=terms, ap_ptr=ap_ptr, ap_col=ap_col, px_ptr=px_ptr, px_col=px_col, c_ptr=c_ptr,
                  c_col=c_col, c_val=c_val, c_nnz=c_nnz, s=s, g=g, diag=diag, den=den, g_t=g_t,
                  t_perm=t_perm, t_rank=t_rank, tile_off=tile_off, tile_ent=tile_ent,
                  tile_maxc=tile_maxc, tile_gmin=tile_gmin, stats=stats, status=status,
@@ -302,13 +304,9 @@ class PathSimEngine:
         first and to balance row shards across ranks."""
         if "row_work" not in self._dev:
             d = self._dev
-            NA, NV = self.typed.n_authors, self.typed.n_mids
+            NA = self.typed.n_authors
             with torch.cuda.device(self.device):
-                terms = self._empty(NA, torch.int64)
-                ncol = self._empty(NV, torch.int32)
-                _lib.call("dps_row_work", _ptr(d["c_ptr"]), _ptr(d["c_col"]), NA, NV, _ptr(ncol),
-                          _ptr(terms), self.stream)
-                terms = terms[:NA]
+                terms = d["row_terms"][:NA]            # from the build's fused walk pass
                 d["row_work"] = terms + (terms.sum() // max(NA, 1)) // 2
         return self._dev["row_work"]
 

@@ -197,6 +197,16 @@ int dps_col_sums(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
 int dps_row_work(const int64_t* c_ptr, const int32_t* c_col, int64_t n_rows, int64_t n_mids,
                  uint32_t* col_count_ws, int64_t* terms, void* stream);
 
+/* A4 fused (what the engine runs every build): s = column sums of C over rows
+ * [0, n_rows) (dps_col_sums), n_v = entries per mid over the author rows
+ * [0, n_authors) (uint32 [n_mids]), then over the author rows g, diag
+ * (nullable), the row work terms[x] = sum_{v in x} n_v (nullable; as
+ * dps_row_work) and stats (nullable) -- two passes over C instead of four. */
+int dps_walks_fused(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                    int64_t n_rows, int64_t n_authors, int64_t n_mids, int64_t* s,
+                    uint32_t* n_v, int64_t* g, int64_t* diag, int64_t* terms, int64_t* stats,
+                    void* stream);
+
 /* ---------------------------------------------------------------------------
  * A5 operand layout, step 1: target relabeling (a pure layout choice; results
  * never depend on it).  Targets are relabeled in ascending global walk g (ties

@@ -1,0 +1,36 @@
+"""The fused walk pass of the build (dps_walks_fused: s, n_v, g, diag, row work
+in two passes over C) against the separate entry points and the C oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fused_walks_match_separate_entry_points():
+    import torch
+    import pathsim_oracle as po
+    from dpathsim import _lib
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_dblp
+    t = synth_dblp(20_000, 60_000, 500, seed=13).typed()
+    eng = build_engine(t)
+    co = po.COracle.from_typed(t)
+    cp, cc, cv, s_o, g_o = co.export()
+    na, nv, nr = t.n_authors, t.n_mids, t.n_rows
+    d = eng._dev
+    assert np.array_equal(d["s"][:nv].cpu().numpy(), s_o[:nv])
+    assert np.array_equal(d["g"][:na].cpu().numpy(), g_o[:na])
+    st = torch.cuda.current_stream().cuda_stream
+    s = torch.empty(nv, dtype=torch.int64, device="cuda")
+    _lib.call("dps_col_sums", d["c_ptr"].data_ptr(), d["c_col"].data_ptr(), d["c_val"].data_ptr(),
+              nr, nv, s.data_ptr(), st)
+    terms = torch.empty(na, dtype=torch.int64, device="cuda")
+    ncol = torch.empty(nv, dtype=torch.int32, device="cuda")
+    _lib.call("dps_row_work", d["c_ptr"].data_ptr(), d["c_col"].data_ptr(), na, nv,
+              ncol.data_ptr(), terms.data_ptr(), st)
+    assert torch.equal(s, d["s"][:nv])
+    assert torch.equal(terms, d["row_terms"][:na])
+    # row work = sum over the row's venues of the author entries per venue
+    n_v = np.bincount(cc[: cp[na]], minlength=nv)
+    expect = np.add.reduceat(n_v[cc[: cp[na]]], cp[:na]) * (np.diff(cp[: na + 1]) > 0)
+    assert np.array_equal(terms.cpu().numpy(), expect)

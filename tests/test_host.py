@@ -218,3 +218,15 @@ def test_cli_arguments():
                 ["--graph", "g", "--synth", "config3", "--all-pairs"]):
         with pytest.raises(SystemExit):
             parse(bad)
+
+
+def test_compat_rejects_a_non_engine_graphframe(tmp_path, dblp_small_tuples):
+    """DPathSim_APVPA's second argument replaces the reference's GraphFrame
+    (DPathSim_APVPA.py:9); anything but a PathSimEngine (or None) is a TypeError,
+    raised before any device work and before the log file is opened."""
+    from dpathsim.compat import DPathSim_APVPA
+    g = Graph.from_tuples(*dblp_small_tuples)
+    log = tmp_path / "run.log"
+    with pytest.raises(TypeError, match="PathSimEngine"):
+        DPathSim_APVPA(g, object(), "author_0", str(log))
+    assert not log.exists()
