@@ -4,7 +4,8 @@
 One "step" = the whole hot path over one synthetic graph already resident in
 HBM: typed incidence extraction -> typed CSR build (distinct) -> SpGEMM C ->
 s, g -> target-tiled C^T -> fused C.C^T + fp64 score + top-k over this rank's
-author rows -> gather of every rank's top-k to rank 0 (RCCL all_gather).
+author rows -> gather of every rank's top-k to rank 0 (one RCCL gather of
+8-byte (count, index) words; rank 0 rescores with its own g).
 value = N_A*(N_A-1) / step time (max over ranks), whole job.
 
 Workload (configs[1] = dblp_large.gexf is absent, .MISSING_LARGE_BLOBS:1):
@@ -56,7 +57,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dpathsim.dist import balanced_bounds, balanced_edges, gather_topk, max_shard, pack_topk
+    from dpathsim.dist import (balanced_bounds, balanced_edges, gather_topk_compact, max_shard,
+                               pack_counts)
     from dpathsim.engine import PathSimEngine
     from dpathsim.synth import CONFIGS, synth_config
 
@@ -96,10 +98,10 @@ def main():
     out = (torch.empty((m, k), dtype=torch.int32, device=dev),
            torch.empty((m, k), dtype=torch.int64, device=dev),
            torch.empty((m, k), dtype=torch.float64, device=dev))
-    packed = torch.empty((m, 2 * k), dtype=torch.int64, device=dev)
+    packed = torch.empty((m, k), dtype=torch.int64, device=dev)
     gathered = None
     if world > 1 and rank == 0:
-        gathered = torch.empty((world * m, 2 * k), dtype=torch.int64, device=dev)
+        gathered = torch.empty((world * m, k), dtype=torch.int64, device=dev)
 
     ev_topk = []
     # every step re-derives the shards from its own C on the device (no host
@@ -124,8 +126,11 @@ def main():
             e1.record()
             ev_topk.append((e0, e1))
         if world > 1:   # one packed buffer per rank, gathered to rank 0 (RCCL)
-            pack_topk(*out, out=packed)
-            gather_topk(packed, NA, world, out=gathered, bounds=bounds)
+            # 8 B per slot on the wire: (count << 32) | index; rank 0 rebuilds
+            # the fp64 scores from its own g (the same exact division)
+            pack_counts(out[0], out[1], out=packed)
+            gather_topk_compact(packed, eng.tensor("den")[:NA], NA, world, out=gathered,
+                                bounds=bounds)
 
     for _ in range(args.warmup):
         step(False)

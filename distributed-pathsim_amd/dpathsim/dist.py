@@ -123,6 +123,61 @@ def gather_topk(parts, n_rows: int, world: int, group=None, out=None, bounds=Non
     return unpack_topk(full)
 
 
+# ------------------------------------------------------ compact (8 B) gather
+def pack_counts(idx: torch.Tensor, cnt: torch.Tensor, out=None):
+    """(idx int32, cnt int64) [R, k] -> int64 [R, k] = (count << 32) | index: the
+    score is NOT sent -- the root recomputes it (:func:`rescore`)."""
+    if out is None:
+        out = torch.empty(idx.shape, dtype=torch.int64, device=idx.device)
+    torch.bitwise_or(cnt.to(torch.int64) << 32, idx.to(torch.int64) & 0xFFFFFFFF, out=out)
+    return out
+
+
+def rescore(packed: torch.Tensor, den: torch.Tensor, row_begin: int = 0):
+    """(idx, cnt, score) from :func:`pack_counts` words of rows row_begin...:
+    score = double(2 cnt) / double(den[x] + den[y]) -- the hot kernel's one fp64
+    division of the same exact integers (DPathSim_APVPA.py:51-52), so the bits
+    are identical -- and 0.0 for zero counts and empty (-1) slots."""
+    idx = (packed & 0xFFFFFFFF).to(torch.int32)
+    cnt = packed >> 32
+    rows = torch.arange(row_begin, row_begin + packed.shape[0], device=packed.device)
+    den = den.to(packed.device)
+    y = idx.to(torch.int64).clamp_min(0)
+    num = (2 * cnt).to(torch.float64)
+    dsum = (den[rows].unsqueeze(1) + den[y]).to(torch.float64)
+    score = torch.where((idx >= 0) & (cnt > 0), num / dsum, torch.zeros_like(num))
+    return idx, cnt, score
+
+
+def gather_topk_compact(parts, den: torch.Tensor, n_rows: int, world: int, group=None,
+                        out=None, bounds=None, dst: int = 0):
+    """As :func:`gather_topk`, with 8 B per slot on the wire: every rank sends
+    (count << 32) | index words; rank ``dst`` rebuilds the scores from its own
+    copy of the denominator term ``den`` (every rank holds all of g).  ``parts``:
+    (idx, cnt[, score]) [max_shard, k] or packed int64 [max_shard, k]."""
+    if bounds is None:
+        bounds = [shard_bounds(n_rows, r, world) for r in range(world)]
+    packed = parts if isinstance(parts, torch.Tensor) else pack_counts(parts[0], parts[1])
+    if world == 1:
+        return rescore(packed[:bounds[0][1] - bounds[0][0]], den)
+    m = max_shard(n_rows, world, bounds)
+    if packed.shape[0] != m:
+        raise ValueError(f"part has {packed.shape[0]} rows, expected max_shard {m}")
+    rank = dist.get_rank(group)
+    nccl = dist.get_backend(group) == "nccl"
+    src = packed.contiguous() if nccl else packed.contiguous().cpu()
+    recv = None
+    if rank == dst:
+        if out is None or not nccl:
+            out = torch.empty((world * m, packed.shape[1]), dtype=torch.int64, device=src.device)
+        recv = list(out.view(world, m, packed.shape[1]).unbind(0))
+    dist.gather(src, gather_list=recv, dst=dst, group=group)
+    if rank != dst:
+        return None
+    full = torch.cat([out[r * m: r * m + (b - a)] for r, (a, b) in enumerate(bounds)])
+    return rescore(full.to(packed.device), den)
+
+
 # ------------------------------------------------------- per-rank shard files
 def write_topk_shard(directory, rank: int, world: int, bounds, parts, k: int) -> str:
     """Write this rank's rows [r0, r1) as ``topk_rank{rank:05d}.npy`` (packed int64

@@ -14,8 +14,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from dpathsim.dist import (balanced_bounds, gather_topk, max_shard, pack_topk, read_topk_shards,
-                           shard_bounds, unpack_topk, write_topk_shard)
+from dpathsim.dist import (balanced_bounds, gather_topk, gather_topk_compact, max_shard,
+                           pack_topk, read_topk_shards, shard_bounds, unpack_topk,
+                           write_topk_shard)
 
 
 @pytest.mark.parametrize("n", [0, 1, 7, 1000, 1_000_003])
@@ -72,16 +73,19 @@ def _worker(rank, world, port, k, result_path, balanced=False):
             p[: r1 - r0] = torch.from_numpy(a)
             parts.append(p)
         res = gather_topk(tuple(parts), na, world, bounds=bounds)
+        # the 8-byte wire format: counts and indices only, scores rebuilt on rank 0
+        g = torch.from_numpy(co.export()[4][:na].astype(np.int64))
+        res8 = gather_topk_compact(tuple(parts[:2]), g, na, world, bounds=bounds)
         shard_dir = result_path + ".shards"
         write_topk_shard(shard_dir, rank, world, bounds or [shard_bounds(na, r, world)
                                                            for r in range(world)], tuple(parts), k)
         dist.barrier()
         if rank != 0:
-            assert res is None          # gathered to rank 0 only
+            assert res is None and res8 is None   # gathered to rank 0 only
         else:
             fi, fc, fs = co.topk(k, 0, na, threads=1)
             ok = True
-            for gi, gc, gs in (res, read_topk_shards(shard_dir)):
+            for gi, gc, gs in (res, res8, read_topk_shards(shard_dir)):
                 ok = ok and (np.array_equal(gi.numpy(), fi) and np.array_equal(gc.numpy(), fc)
                              and np.array_equal(gs.numpy().view(np.int64), fs.view(np.int64)))
             with open(result_path, "w") as f:
@@ -97,6 +101,22 @@ def test_gloo_gather_equals_single_rank(tmp_path, world, balanced):
     mp.start_processes(_worker, args=(world, _free_port(), 10, str(out), balanced), nprocs=world,
                        join=True, start_method="spawn")
     assert out.read_text() == "ok"
+
+
+def test_compact_rescore_matches_kernel_division():
+    """rescore() rebuilds score = double(2 cnt) / double(den[x] + den[y]) bit for
+    bit (the oracle's scores), 0.0 for zero counts and -1 slots."""
+    import pathsim_oracle as po
+    from dpathsim.dist import pack_counts, rescore
+    from dpathsim.synth import synth_dblp
+    t = synth_dblp(3000, 9000, 150, seed=4).typed()
+    co = po.COracle.from_typed(t)
+    g = torch.from_numpy(co.export()[4][: t.n_authors].astype(np.int64))
+    oi, oc, os_ = co.topk(10, 100, 700, threads=1)
+    oi[5, 9], oc[5, 9], os_[5, 9] = -1, 0, 0.0            # an empty slot
+    i2, c2, s2 = rescore(pack_counts(torch.from_numpy(oi), torch.from_numpy(oc)), g, 100)
+    assert np.array_equal(i2.numpy(), oi) and np.array_equal(c2.numpy(), oc)
+    assert np.array_equal(s2.numpy().view(np.int64), os_.view(np.int64))
 
 
 def test_pack_roundtrip():
