@@ -49,6 +49,19 @@ def test_balanced_bounds_partition_and_balance(world):
     assert balanced_bounds(torch.zeros(0, dtype=torch.int64), world) == [(0, 0)] * world
 
 
+@pytest.mark.parametrize("world", [1, 2, 5, 8])
+def test_balanced_edges_match_bounds(world):
+    """bench.py re-derives the shards inside the timed step as a tensor
+    (balanced_edges, nothing read back); it must equal the host bounds."""
+    from dpathsim.dist import balanced_edges
+    rng = np.random.default_rng(3 + world)
+    w = torch.from_numpy(rng.pareto(1.1, 50_000).astype(np.int64) + 1)
+    e = balanced_edges(w, world).tolist()
+    b = balanced_bounds(w, world)
+    assert [(e[r], e[r + 1]) for r in range(world)] == b
+    assert balanced_edges(torch.zeros(0, dtype=torch.int64), world).tolist() == [0] * (world + 1)
+
+
 def _worker(rank, world, port, k, result_path, balanced=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
