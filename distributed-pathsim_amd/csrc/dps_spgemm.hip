@@ -431,6 +431,25 @@ __global__ __launch_bounds__(kBlock) void k_mid_of_entry(const int64_t* __restri
     mids[j] = vp[ap_col[j]];
 }
 
+// Paper -> mid map straight from the typed PX pairs (no PX CSR): with at most
+// one raw PX edge per paper (the single-mid case, decided on the host) the
+// pairs are already distinct and every paper is written at most once.
+__global__ __launch_bounds__(kBlock) void k_paper_mid_pairs(const int32_t* __restrict__ px_paper,
+                                                            const int32_t* __restrict__ px_mid,
+                                                            int64_t cap, const int64_t* n_dev,
+                                                            int32_t* __restrict__ vp) {
+  const int64_t n = n_dev ? min(*n_dev, cap) : cap;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kBlock)
+    vp[px_paper[i]] = px_mid[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_i32(int32_t* __restrict__ a, int64_t n, int32_t v) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kBlock)
+    a[i] = v;
+}
+
 // After the segmented unique: drop a trailing INT_MAX head (papers without a
 // mid) from each row's count.
 __global__ __launch_bounds__(kBlock) void k_drop_none(const int32_t* __restrict__ mids,
@@ -505,10 +524,35 @@ size_t dps_spgemm_single_workspace_size(int64_t n_out_rows, int64_t nnz_ap, int6
   return s + 1024;
 }
 
+int dps_paper_mid_map(const int32_t* px_paper, const int32_t* px_mid, int64_t n_px_cap,
+                      const int64_t* n_px_dev, int64_t n_papers, int32_t* vp, void* stream) {
+  DPS_REQUIRE(n_px_cap >= 0 && n_papers >= 0, DPS_ERR_INVALID, "negative size");
+  DPS_REQUIRE(n_papers == 0 || vp, DPS_ERR_INVALID, "null vp");
+  auto st = static_cast<hipStream_t>(stream);
+  if (n_papers == 0) return DPS_OK;
+  k_fill_i32<<<grid_for(n_papers, kBlock), kBlock, 0, st>>>(vp, n_papers, INT_MAX);
+  DPS_LAUNCHED();
+  if (n_px_cap == 0) return DPS_OK;
+  DPS_REQUIRE(px_paper && px_mid, DPS_ERR_INVALID, "null PX pairs");
+  k_paper_mid_pairs<<<grid_for(n_px_cap, kBlock), kBlock, 0, st>>>(px_paper, px_mid, n_px_cap,
+                                                                   n_px_dev, vp);
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
 int dps_spgemm_single(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_out_rows,
                       int64_t nnz_ap_cap, const int64_t* px_ptr, const int32_t* px_col,
                       int64_t n_papers, int64_t n_mids, int64_t* c_ptr, int32_t* c_col,
                       int32_t* c_val, int64_t* c_nnz, void* ws, size_t ws_bytes, void* stream) {
+  return dps_spgemm_single_map(ap_ptr, ap_col, n_out_rows, nnz_ap_cap, nullptr, px_ptr, px_col,
+                               n_papers, n_mids, c_ptr, c_col, c_val, c_nnz, ws, ws_bytes, stream);
+}
+
+int dps_spgemm_single_map(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_out_rows,
+                          int64_t nnz_ap_cap, const int32_t* vp_in, const int64_t* px_ptr,
+                          const int32_t* px_col, int64_t n_papers, int64_t n_mids,
+                          int64_t* c_ptr, int32_t* c_col, int32_t* c_val, int64_t* c_nnz,
+                          void* ws, size_t ws_bytes, void* stream) {
   DPS_REQUIRE(n_out_rows >= 0 && nnz_ap_cap >= 0, DPS_ERR_INVALID, "negative size");
   DPS_REQUIRE(c_ptr && c_nnz, DPS_ERR_INVALID, "null output");
   DPS_REQUIRE(!c_col == !c_val, DPS_ERR_INVALID, "c_col and c_val must both be set (numeric)");
@@ -531,7 +575,10 @@ int dps_spgemm_single(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_ou
   DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "spgemm_single workspace carve failed");
   if (c_col == nullptr) {   // symbolic: map, segmented sort + unique, scan
     if (n_out_rows > 0) {
-      if (n_papers > 0) {
+      if (vp_in) {
+        vp = const_cast<int32_t*>(vp_in);
+      } else if (n_papers > 0) {
+        DPS_REQUIRE(px_ptr && px_col, DPS_ERR_INVALID, "px_ptr / px_col (or vp) required");
         k_paper_mid<<<grid_for(n_papers, kBlock), kBlock, 0, st>>>(px_ptr, px_col, n_papers, vp);
         DPS_LAUNCHED();
       }

@@ -368,6 +368,30 @@ __device__ __forceinline__ void walk_strips(const BlockRows& R, int nl, uint32_t
   }
 }
 
+// perm = inverse of rank, and in the same pass over the rows (coalesced row
+// offsets) the entries per part, reduced in an LDS histogram per block (one
+// global atomic per part and block); n_parts <= kPartLds.
+constexpr int kPartLds = 8192;
+__global__ __launch_bounds__(kBlock) void k_invert_and_parts(const int32_t* __restrict__ rank,
+                                                             const int64_t* __restrict__ c_ptr,
+                                                             int64_t n, int labels_per_block,
+                                                             int n_parts, int32_t* __restrict__ perm,
+                                                             uint32_t* __restrict__ part_n) {
+  __shared__ uint32_t h[kPartLds];
+  for (int i = threadIdx.x; i < n_parts; i += kBlock) h[i] = 0;
+  __syncthreads();
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int64_t lab = rank ? static_cast<int64_t>(rank[i]) : i;
+    if (rank) perm[lab] = static_cast<int32_t>(i);
+    const uint32_t len = static_cast<uint32_t>(c_ptr[i + 1] - c_ptr[i]);
+    if (len) atomicAdd(&h[lab / labels_per_block], len);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n_parts; i += kBlock)
+    if (h[i]) atomicAdd(&part_n[i], h[i]);
+}
+
 // Entries per part (sum of its labels' row lengths), one atomic per wave.
 __global__ __launch_bounds__(kBlock) void k_part_entries(const int64_t* __restrict__ c_ptr,
                                                          const int32_t* __restrict__ perm,
@@ -767,7 +791,13 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   DPS_REQUIRE(nblk * S < INT32_MAX, DPS_ERR_OVERFLOW, "too many tile-build blocks");
   const bool p16 = shift <= kP16MaxShift;   // counts and offsets are in entries
   const uint32_t per16 = p16 ? 8u : 4u;
-  if (blk && t_rank && n_targets > 0) {
+  const bool fused_parts = blk && n_targets > 0 && nblk <= kPartLds;
+  if (fused_parts) {
+    DPS_HIP_RET(hipMemsetAsync(part_n, 0, (nblk + 1) * sizeof(uint32_t), st));
+    k_invert_and_parts<<<grid_for(n_targets, kBlock, 1024), kBlock, 0, st>>>(
+        t_rank, c_ptr, n_targets, lpb, static_cast<int>(nblk), perm, part_n);
+    DPS_LAUNCHED();
+  } else if (blk && t_rank && n_targets > 0) {
     k_tile_invert<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(t_rank, n_targets, perm);
     DPS_LAUNCHED();
   }
@@ -778,11 +808,13 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     DPS_HIP_RET(hipMemsetAsync(cntp, 0, (np + 1) * sizeof(uint32_t), st));
     DPS_HIP_RET(hipMemsetAsync(mxp, 0, (np + 1) * sizeof(uint32_t), st));
     DPS_HIP_RET(hipMemsetAsync(curp, 0, (np + 1) * sizeof(uint32_t), st));
-    DPS_HIP_RET(hipMemsetAsync(part_n, 0, (nblk + 1) * sizeof(uint32_t), st));
-    if (n_targets > 0) {
-      k_part_entries<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(c_ptr, perm_or_null, n_targets,
-                                                                     lpb, part_n);
-      DPS_LAUNCHED();
+    if (!fused_parts) {
+      DPS_HIP_RET(hipMemsetAsync(part_n, 0, (nblk + 1) * sizeof(uint32_t), st));
+      if (n_targets > 0) {
+        k_part_entries<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(c_ptr, perm_or_null,
+                                                                       n_targets, lpb, part_n);
+        DPS_LAUNCHED();
+      }
     }
     if (tile_maxc) DPS_HIP_RET(hipMemsetAsync(tile_maxc + nb, 0, sizeof(uint32_t), st));
     if (n_targets > 0 && nb > 0) {

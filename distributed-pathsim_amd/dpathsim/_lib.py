@@ -49,6 +49,9 @@ SIGNATURES = {
     "dps_spgemm_single_workspace_size": (_sz, [_i64, _i64, _i64]),
     "dps_spgemm_single": (C.c_int, [_p, _p, _i64, _i64, _p, _p, _i64, _i64, _p, _p, _p, _p, _p,
                                     _sz, _p]),
+    "dps_spgemm_single_map": (C.c_int, [_p, _p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p,
+                                        _p, _p, _sz, _p]),
+    "dps_paper_mid_map": (C.c_int, [_p, _p, _i64, _p, _i64, _p, _p]),
     "dps_mid_walks": (C.c_int, [_p, _p, _i64, _p, _p, _i64, _i64, _p, _p, _p]),
     "dps_global_walks": (C.c_int, [_p, _p, _p, _i64, _p, _p, _p, _p, _p]),
     "dps_row_work": (C.c_int, [_p, _p, _i64, _i64, _p, _p, _p]),

@@ -168,10 +168,20 @@ class PathSimEngine:
             ap_nnz = self._empty(1, torch.int64)
             _lib.call("dps_csr_build", _ptr(ap_r), _ptr(ap_c), E, _ptr(n_ap), NR, _ptr(ap_ptr),
                       _ptr(ap_col), _ptr(ap_nnz), _ptr(ws), ws.numel(), st)
-            px_ptr, px_col = self._empty(NP + 1, torch.int64), self._empty(E, torch.int32)
-            px_nnz = self._empty(1, torch.int64)
-            _lib.call("dps_csr_build", _ptr(px_r), _ptr(px_c), E, _ptr(n_px), NP, _ptr(px_ptr),
-                      _ptr(px_col), _ptr(px_nnz), _ptr(ws), ws.numel(), st)
+            single = bnd.max_mids_per_paper <= 1
+            if single:
+                # at most one raw PX edge per paper: the PX pairs are already
+                # distinct -- a paper -> mid map replaces the PX CSR
+                vp = self._empty(NP, torch.int32)
+                _lib.call("dps_paper_mid_map", _ptr(px_r), _ptr(px_c), E, _ptr(n_px), NP, _ptr(vp),
+                          st)
+                px_ptr = px_col = None
+                px_nnz = n_px
+            else:
+                px_ptr, px_col = self._empty(NP + 1, torch.int64), self._empty(E, torch.int32)
+                px_nnz = self._empty(1, torch.int64)
+                _lib.call("dps_csr_build", _ptr(px_r), _ptr(px_c), E, _ptr(n_px), NP, _ptr(px_ptr),
+                          _ptr(px_col), _ptr(px_nnz), _ptr(ws), ws.numel(), st)
             del ap_r, ap_c, px_r, px_c
             mark("csr")
             # A3: SpGEMM C = W_AP . W_PX over EVERY AP row (author rows [0, NA)
@@ -183,14 +193,15 @@ class PathSimEngine:
             c_ptr, c_nnz = self._empty(NR + 1, torch.int64), self._empty(2, torch.int64)
             sp_status = self._empty(1, torch.int32)
             c_col, c_val = self._empty(cap, torch.int32), self._empty(cap, torch.int32)
-            if bnd.max_mids_per_paper <= 1:
+            if single:
                 sws = self._ws(_lib.size("dps_spgemm_single_workspace_size", NR, E, NP))
                 sp_status.zero_()
                 for numeric in (False, True):
-                    _lib.call("dps_spgemm_single", _ptr(ap_ptr), _ptr(ap_col), NR, E, _ptr(px_ptr),
-                              _ptr(px_col), NP, NV, _ptr(c_ptr), _ptr(c_col) if numeric else None,
+                    _lib.call("dps_spgemm_single_map", _ptr(ap_ptr), _ptr(ap_col), NR, E, _ptr(vp),
+                              None, None, NP, NV, _ptr(c_ptr), _ptr(c_col) if numeric else None,
                               _ptr(c_val) if numeric else None, _ptr(c_nnz), _ptr(sws),
                               sws.numel(), st)
+                del vp
             else:
                 sws = self._ws(_lib.size("dps_spgemm_hash_workspace_size", NR, bnd.max_row_expand))
                 for numeric in (False, True):

@@ -166,6 +166,21 @@ int dps_spgemm_single(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_ou
                       int64_t n_papers, int64_t n_mids, int64_t* c_ptr, int32_t* c_col,
                       int32_t* c_val, int64_t* c_nnz, void* ws, size_t ws_bytes, void* stream);
 
+/* The same with the paper -> mid map given (vp int32 [n_papers], INT_MAX = no
+ * mid); px_ptr / px_col are then unused (may be NULL).  Same workspace. */
+int dps_spgemm_single_map(const int64_t* ap_ptr, const int32_t* ap_col, int64_t n_out_rows,
+                          int64_t nnz_ap_cap, const int32_t* vp, const int64_t* px_ptr,
+                          const int32_t* px_col, int64_t n_papers, int64_t n_mids,
+                          int64_t* c_ptr, int32_t* c_col, int32_t* c_val, int64_t* c_nnz,
+                          void* ws, size_t ws_bytes, void* stream);
+
+/* Paper -> mid map from the typed PX pairs of dps_extract_incidence (capacity
+ * n_px_cap, count in the device scalar n_px_dev if non-NULL), without a PX CSR:
+ * valid when no paper has two raw PX edges (the single-mid case; the distinct
+ * of :86 is then a no-op).  vp int32 [n_papers], INT_MAX where no mid. */
+int dps_paper_mid_map(const int32_t* px_paper, const int32_t* px_mid, int64_t n_px_cap,
+                      const int64_t* n_px_dev, int64_t n_papers, int32_t* vp, void* stream);
+
 /* ---------------------------------------------------------------------------
  * A4. Global walk ingredients.
  * dps_mid_walks: s[v] = sum over ALL AP rows r of C[r,v]
