@@ -38,8 +38,18 @@ for setting in os.environ.get("AB_ENV", "").split(";"):
         order = torch.argsort(w, descending=True, stable=True)
         torch.cuda.synchronize()
         walls.append((time.perf_counter() - t0) * 1e3)
+    # host enqueue time of one build (no sync inside): below the device time
+    # the GPU never waits for the host, so a graph capture would not shorten it
+    enq = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.build(check=False)
+        enq.append((time.perf_counter() - t0) * 1e3)
+        torch.cuda.synchronize()
     med = {k: float(np.median([p[k] for p in phases])) for k in phases[0]}
     print(json.dumps({"env": env, "phase_ms": med, "phase_total_ms": sum(med.values()),
-                      "build_plus_plan_wall_ms": float(np.median(walls))}), flush=True)
+                      "build_plus_plan_wall_ms": float(np.median(walls)),
+                      "host_enqueue_ms": float(np.median(enq))}), flush=True)
     for k in env:
         os.environ.pop(k)
