@@ -18,7 +18,11 @@ import torch
 from dpathsim.engine import PathSimEngine
 from dpathsim.synth import synth_config
 
-t = synth_config(os.environ.get("AB_CONFIG", "config3")).typed()
+from dpathsim.graph import METAPATHS
+from dpathsim.synth import CONFIGS
+
+_cfg = os.environ.get("AB_CONFIG", "config3")
+t = synth_config(_cfg).typed(METAPATHS[CONFIGS[_cfg][3]])
 reps = int(os.environ.get("AB_REPS", "5"))
 eng = PathSimEngine(t, tile_w=int(os.environ.get("AB_W", "8192"))).upload()
 for setting in os.environ.get("AB_ENV", "").split(";"):
