@@ -287,6 +287,58 @@ BucketPlan bucket_plan(int64_t cap, int64_t n_rows) {
   return P;
 }
 
+// Column sums (and author-entry counts) for more mids than one LDS range: one
+// pass over the entries, each block reducing a chunk of kColChunk entries in an
+// LDS hash table (open addressing; a chunk has at most kColChunk distinct mids,
+// so the 2x-sized table never fills), then one global atomic per (block, mid)
+// -- instead of re-reading every entry once per 6144-mid range (config4: 33
+// ranges of 200k topics).
+constexpr int kColChunk = 4096;
+constexpr int kColSlots = 2 * kColChunk;
+
+__device__ __forceinline__ uint32_t col_slot(uint32_t v) {
+  return (v * 2654435761u) >> (32 - 13);   // kColSlots = 2^13
+}
+
+__global__ __launch_bounds__(kBlock) void k_col_sums_hash(const int64_t* __restrict__ c_ptr,
+                                                          const int32_t* __restrict__ c_col,
+                                                          const int32_t* __restrict__ c_val,
+                                                          int64_t n_rows,
+                                                          unsigned long long* __restrict__ s,
+                                                          int64_t n_count_rows,
+                                                          unsigned* __restrict__ n_v) {
+  __shared__ int32_t key[kColSlots];
+  __shared__ unsigned long long sum[kColSlots];
+  __shared__ unsigned cnt[kColSlots];
+  const int64_t b0 = c_ptr[0], nnz = c_ptr[n_rows] - b0;
+  const int64_t ncnt = n_v ? c_ptr[n_count_rows] - b0 : 0;
+  for (int64_t j0 = static_cast<int64_t>(blockIdx.x) * kColChunk; j0 < nnz;
+       j0 += static_cast<int64_t>(gridDim.x) * kColChunk) {
+    for (int t = threadIdx.x; t < kColSlots; t += kBlock) { key[t] = -1; sum[t] = 0; cnt[t] = 0; }
+    __syncthreads();
+    const int64_t j1 = min(j0 + kColChunk, nnz);
+    for (int64_t j = j0 + threadIdx.x; j < j1; j += kBlock) {
+      const int32_t v = c_col[b0 + j];
+      uint32_t h = col_slot(static_cast<uint32_t>(v));
+      for (;;) {
+        const int32_t old = atomicCAS(&key[h], -1, v);
+        if (old == -1 || old == v) break;
+        h = (h + 1) & (kColSlots - 1);
+      }
+      atomicAdd(&sum[h], static_cast<unsigned long long>(c_val[b0 + j]));
+      if (j < ncnt) atomicAdd(&cnt[h], 1u);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < kColSlots; t += kBlock) {
+      const int32_t v = key[t];
+      if (v < 0) continue;
+      atomicAdd(&s[v], sum[t]);
+      if (n_v && cnt[t]) atomicAdd(&n_v[v], cnt[t]);
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Segmented sort + unique (+ run lengths).
 // Tiny segments (2..16): one lane each, a 16-input bitonic network in registers.
@@ -1239,11 +1291,14 @@ int dps_walks_fused(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c
   if (n_mids > 0) {
     DPS_HIP_RET(hipMemsetAsync(s, 0, n_mids * sizeof(int64_t), st));
     DPS_HIP_RET(hipMemsetAsync(n_v, 0, n_mids * sizeof(uint32_t), st));
-    if (n_rows > 0) {
-      const unsigned ny = static_cast<unsigned>((n_mids + kSumLds - 1) / kSumLds);
-      k_col_sums<<<dim3(ny > 1 ? 256 : 512, ny), kBlock, 0, st>>>(
-          c_ptr, c_col, c_val, n_rows, n_mids, reinterpret_cast<unsigned long long*>(s),
-          n_authors, n_v);
+    if (n_rows > 0 && n_mids > kSumLds) {
+      k_col_sums_hash<<<1024, kBlock, 0, st>>>(c_ptr, c_col, c_val, n_rows,
+                                               reinterpret_cast<unsigned long long*>(s),
+                                               n_authors, n_v);
+      DPS_LAUNCHED();
+    } else if (n_rows > 0) {
+      k_col_sums<<<512, kBlock, 0, st>>>(c_ptr, c_col, c_val, n_rows, n_mids,
+                                         reinterpret_cast<unsigned long long*>(s), n_authors, n_v);
       DPS_LAUNCHED();
     }
   }
@@ -1263,9 +1318,13 @@ int dps_col_sums(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   if (n_mids == 0) return DPS_OK;
   DPS_HIP_RET(hipMemsetAsync(s, 0, n_mids * sizeof(int64_t), st));
   if (n_rows == 0) return DPS_OK;
-  const unsigned ny = static_cast<unsigned>((n_mids + kSumLds - 1) / kSumLds);
-  k_col_sums<<<dim3(ny > 1 ? 256 : 512, ny), kBlock, 0, st>>>(
-      c_ptr, c_col, c_val, n_rows, n_mids, reinterpret_cast<unsigned long long*>(s), 0, nullptr);
+  if (n_mids > kSumLds) {
+    k_col_sums_hash<<<1024, kBlock, 0, st>>>(c_ptr, c_col, c_val, n_rows,
+                                             reinterpret_cast<unsigned long long*>(s), 0, nullptr);
+  } else {
+    k_col_sums<<<512, kBlock, 0, st>>>(c_ptr, c_col, c_val, n_rows, n_mids,
+                                       reinterpret_cast<unsigned long long*>(s), 0, nullptr);
+  }
   DPS_LAUNCHED();
   return DPS_OK;
 }

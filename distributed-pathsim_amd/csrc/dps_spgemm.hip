@@ -32,6 +32,7 @@ constexpr int kLaneCap = 16;        // expansion a lane sorts in registers
 constexpr int kHashSlots = 8192;    // LDS hash slots of the workgroup path
 constexpr int kHashCap = 4096;      // expansion the LDS hash takes (load <= 1/2)
 constexpr int kHugeBlocks = 32;     // workgroups (and scratch regions) of the L > 4096 path
+constexpr int kRankSortMax = 1024;  // distinct keys of a row sorted by ranking (numeric pass)
 
 __device__ __forceinline__ int64_t out_row(const int32_t* rows, int64_t i) {
   return rows ? static_cast<int64_t>(rows[i]) : i;
@@ -304,6 +305,40 @@ __global__ __launch_bounds__(kBlock) void k_hash_long(
       const int nu = n_occ;
       if (!kNumeric) {
         if (threadIdx.x == 0) u[i] = static_cast<uint32_t>(nu);
+      } else if (nu <= kRankSortMax) {
+        // rank sort of the (distinct) keys: every occupied slot's position is
+        // the number of smaller keys -- two barriers instead of log^2 phases
+        int32_t key[kRankSortMax / kBlock], cnt[kRankSortMax / kBlock];
+#pragma unroll
+        for (int q = 0; q < kRankSortMax / kBlock; ++q) {
+          const int t = threadIdx.x + q * kBlock;
+          key[q] = t < nu ? hkey[occ[t]] : INT_MAX;
+          cnt[q] = t < nu ? hcnt[occ[t]] : 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kRankSortMax / kBlock; ++q) {
+          const int t = threadIdx.x + q * kBlock;
+          if (t < nu) occ[t] = key[q];                 // occ now holds the keys
+        }
+        __syncthreads();
+        const int64_t o = c_ptr[i];
+#pragma unroll
+        for (int q = 0; q < kRankSortMax / kBlock; ++q) {
+          const int t = threadIdx.x + q * kBlock;
+          if (t >= nu) continue;
+          int r = 0;
+          for (int w = 0; w < nu; ++w) r += occ[w] < key[q] ? 1 : 0;
+          c_col[o + r] = key[q];
+          c_val[o + r] = cnt[q];
+        }
+        __syncthreads();
+        // restore the slot list for the reset below
+        for (int t = threadIdx.x; t < nu; t += kBlock) {
+          uint32_t h = hash_slot(static_cast<uint32_t>(occ[t]));
+          while (hkey[h] != occ[t]) h = (h + 1) & (kHashSlots - 1);
+          occ[t] = static_cast<int32_t>(h);
+        }
       } else {
         // sort the occupied slots by their key, then write (key, count)
         int n2 = 1;
