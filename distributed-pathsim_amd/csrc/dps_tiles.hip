@@ -468,7 +468,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
   const BlockRows R{rel_s, d_s};
   const int nl = static_cast<int>(l1 - l0);
   const bool do_g = gmin && sb == 0;
-  const uint32_t n = stage_rows(c_ptr, perm, do_g ? g : nullptr, l0, l1, R, wsum, &gmin_s);
+  [[maybe_unused]] const uint32_t n = stage_rows(c_ptr, perm, do_g ? g : nullptr, l0, l1, R, wsum, &gmin_s);
   DPS_DASSERT(n == part_n[part]);
   if (sr.e1 - sr.e0 <= kMaxStrips * kWave) strip_table(R, nl, sr.e0, sr.e1, tab_s);
   const uint32_t lab0 = static_cast<uint32_t>(l0);

@@ -52,6 +52,10 @@ SIGNATURES = {
     "dps_spgemm_single_map": (C.c_int, [_p, _p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p,
                                         _p, _p, _sz, _p]),
     "dps_paper_mid_map": (C.c_int, [_p, _p, _i64, _p, _i64, _p, _p]),
+    "dps_gexf_open": (_p, [C.c_char_p, _p]),
+    "dps_gexf_info": (_i64, [_p, C.c_int32]),
+    "dps_gexf_export": (C.c_int, [_p] + [_p] * 15),
+    "dps_gexf_close": (None, [_p]),
     "dps_mid_walks": (C.c_int, [_p, _p, _i64, _p, _p, _i64, _i64, _p, _p, _p]),
     "dps_global_walks": (C.c_int, [_p, _p, _p, _i64, _p, _p, _p, _p, _p]),
     "dps_row_work": (C.c_int, [_p, _p, _i64, _i64, _p, _p, _p]),

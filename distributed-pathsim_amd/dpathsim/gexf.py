@@ -52,15 +52,31 @@ def _convert(value, atype):
     return value
 
 
-def read_gexf(path, with_stats=False):
-    """Parse ``path`` into a :class:`Graph` (strings interned, arrays int32)."""
+def _intern(values, missing):
+    """Objects -> (int32 codes in first-appearance order, distinct values);
+    ``missing`` (KeyError / None markers) -> -1."""
+    table, names = {}, []
+    codes = np.empty(len(values), dtype=np.int64)
+    for i, v in enumerate(values):
+        if v is missing:
+            codes[i] = -1
+            continue
+        c = table.get(v)
+        if c is None:
+            c = table[v] = len(names)
+            names.append(v)
+        codes[i] = c
+    return codes, names
+
+
+def _parse_python(path):
+    """The iterparse loop (the reference semantics, any GEXF ElementTree reads)."""
     node_index = {}
     node_ids, labels, types = [], [], []
     node_attr, edge_attr = {}, {}
     attr_class = None
     directed = True
     e_src, e_dst, e_rel, e_key = [], [], [], []
-    e_label_missing = []
     depth_nodes = 0
     cur = None          # dict for the element being assembled
     cur_kind = None
@@ -132,43 +148,140 @@ def read_gexf(path, with_stats=False):
         elif tag == "nodes":
             depth_nodes -= 1
 
+    tcodes, tvals = _intern(types, KeyError)
+    rcodes, rnames = _intern(e_rel, KeyError)
+    return dict(directed=directed, node_ids=node_ids, labels=labels, node_index=node_index,
+                tcodes=tcodes, tvals=tvals, src=np.asarray(e_src, dtype=np.int64),
+                dst=np.asarray(e_dst, dtype=np.int64), rcodes=rcodes, rnames=rnames,
+                key=e_key.__getitem__)
+
+
+def _parse_native(path):
+    """libdpathsim's mmap'ed scanner (dps_gexf.cpp); None when the file is
+    outside its subset (the Python loop then reports the reference's error)."""
+    import ctypes as C
+    from . import _lib
+    try:
+        lib = _lib.load()
+    except _lib.DPSLibraryError:
+        return None
+    st = C.c_int32(1)
+    h = lib.dps_gexf_open(str(path).encode(), C.byref(st))
+    if not h or st.value != 0:
+        return None
+    try:
+        n, m, nt, nr = (lib.dps_gexf_info(h, w) for w in range(4))
+        directed = bool(lib.dps_gexf_info(h, 4))
+        nb_id, nb_lab, nb_t, nb_r, nb_k = (lib.dps_gexf_info(h, w) for w in range(5, 10))
+        id_off, lab_off = np.empty(n + 1, np.int64), np.empty(n + 1, np.int64)
+        t_off, r_off = np.empty(nt + 1, np.int64), np.empty(nr + 1, np.int64)
+        id_buf, lab_buf = np.empty(max(nb_id, 1), np.uint8), np.empty(max(nb_lab, 1), np.uint8)
+        t_buf, r_buf = np.empty(max(nb_t, 1), np.uint8), np.empty(max(nb_r, 1), np.uint8)
+        lab_null = np.empty(max(n, 1), np.uint8)
+        tcodes = np.empty(max(n, 1), np.int32)
+        src, dst = np.empty(max(m, 1), np.int32), np.empty(max(m, 1), np.int32)
+        rcodes, koff = np.empty(max(m, 1), np.int32), np.empty(max(m, 1), np.int64)
+        kbuf = np.empty(max(nb_k, 1), np.uint8)
+        ptr = lambda a: a.ctypes.data
+        lib.dps_gexf_export(h, ptr(id_off), ptr(id_buf), ptr(lab_off), ptr(lab_buf), ptr(lab_null),
+                            ptr(tcodes), ptr(t_off), ptr(t_buf), ptr(src), ptr(dst), ptr(rcodes),
+                            ptr(koff), ptr(kbuf), ptr(r_off), ptr(r_buf))
+    finally:
+        lib.dps_gexf_close(h)
+
+    def strings(buf, off, k):
+        raw = buf[: off[k]].tobytes()
+        if raw.isascii():            # byte offsets are character offsets
+            text = raw.decode("ascii")
+            o = off.tolist()
+            return [text[o[i]:o[i + 1]] for i in range(k)]
+        o = off.tolist()
+        return [raw[o[i]:o[i + 1]].decode("utf-8") for i in range(k)]
+
+    node_ids = strings(id_buf, id_off, n)
+    labels = strings(lab_buf, lab_off, n)
+    for i in np.flatnonzero(lab_null[:n]).tolist():
+        labels[i] = None
+    return dict(directed=directed, node_ids=node_ids, labels=labels,
+                node_index=dict(zip(node_ids, range(n))), tcodes=tcodes[:n].astype(np.int64),
+                tvals=strings(t_buf, t_off, nt), src=src[:m].astype(np.int64),
+                dst=dst[:m].astype(np.int64), rcodes=rcodes[:m].astype(np.int64),
+                rnames=strings(r_buf, r_off, nr), key=lambda j: _key_at(kbuf, koff, j))
+
+
+def _key_at(buf, off, j):
+    """Edge j's id (bytes) from the native key buffer, None when it has none."""
+    o = int(off[j])
+    if o < 0:
+        return None
+    e = o
+    while buf[e] != 0:
+        e += 1
+    return buf[o:e].tobytes()
+
+
+def _first_appearance(codes):
+    """codes (>= 0) -> (dense ids numbered in order of first appearance, the
+    original code of each dense id)."""
+    if len(codes) == 0:
+        return np.zeros(0, np.int32), np.zeros(0, np.int64)
+    u, first, inv = np.unique(codes, return_index=True, return_inverse=True)
+    rank = np.empty(len(u), np.int64)
+    rank[np.argsort(first, kind="stable")] = np.arange(len(u))
+    return rank[inv].astype(np.int32), u[np.argsort(first, kind="stable")]
+
+
+def read_gexf(path, with_stats=False, native=None):
+    """Parse ``path`` into a :class:`Graph` (strings interned, arrays int32).
+
+    The per-element scan runs natively (``dps_gexf_open``, an mmap'ed scanner
+    in libdpathsim) when the library is present and the file is inside its
+    subset, else in the Python iterparse loop; both feed the same networkx
+    key-collapse and ordering below.  ``native``: force one (True / False)."""
+    P = None
+    if native is not False:
+        P = _parse_native(path)
+        if P is None and native is True:
+            raise RuntimeError("native GEXF scan unavailable or outside its subset")
+    if P is None:
+        P = _parse_python(path)
+    node_ids, labels, node_index = P["node_ids"], P["labels"], P["node_index"]
     n = len(node_ids)
-    for i in range(n):
-        if types[i] is KeyError:
-            raise KeyError("node_type")
-    src = np.asarray(e_src, dtype=np.int64)
-    dst = np.asarray(e_dst, dtype=np.int64)
+    tcodes = P["tcodes"]
+    if n and (tcodes < 0).any():
+        raise KeyError("node_type")
+    src, dst = P["src"], P["dst"]
+    rel = P["rcodes"].copy()
+    key_of = P["key"]
     m = len(src)
-    if not directed and m:
+    if not P["directed"] and m:
         a, b = np.minimum(src, dst), np.maximum(src, dst)
         src, dst = a, b
     # multigraph key collapse: (src, dst, id) repeated -> the last data wins, first position kept
     keep = np.ones(m, dtype=bool)
-    rel = list(e_rel)
     if m:
         pair = src * n + dst
         order = np.argsort(pair, kind="stable")
         ps = pair[order]
         dup_pairs = np.flatnonzero(ps[1:] == ps[:-1])
         if len(dup_pairs):
-            # only pairs that really repeat need the per-key Python check
+            # only pairs that really repeat need the per-key check
             seen = {}
             cand = np.unique(np.concatenate([order[dup_pairs], order[dup_pairs + 1]]))
             for j in sorted(cand.tolist()):
-                kid = e_key[j]
+                kid = key_of(j)
                 if kid is None:
                     continue
                 key = (int(src[j]), int(dst[j]), kid)
                 if key in seen:
                     # networkx MultiGraph.add_edge does datadict.update(attr): a
                     # repeat without a label keeps the earlier one
-                    if rel[j] is not KeyError:
+                    if rel[j] >= 0:
                         rel[seen[key]] = rel[j]
                     keep[j] = False
                 else:
                     seen[key] = j
         # adjacency order: by source node order, then first insertion of the pair
-        first_seen = np.empty(m, dtype=np.int64)
         _, inv = np.unique(pair, return_inverse=True)
         first_pos = np.full(inv.max() + 1 if m else 0, m, dtype=np.int64)
         np.minimum.at(first_pos, inv, np.arange(m))
@@ -178,24 +291,14 @@ def read_gexf(path, with_stats=False):
         sel = sel[ordr]
     else:
         sel = np.zeros(0, dtype=np.int64)
-    rel_sel = [rel[j] for j in sel.tolist()]
-    for r in rel_sel:
-        if r is KeyError:
-            raise KeyError("label")
-    tnames, tmap = [], {}
-    tidx = np.empty(n, dtype=np.int32)
-    for i, t in enumerate(types):
-        if t not in tmap:
-            tmap[t] = len(tnames)
-            tnames.append(t)
-        tidx[i] = tmap[t]
-    rnames, rmap = [], {}
-    ridx = np.empty(len(rel_sel), dtype=np.int32)
-    for j, r in enumerate(rel_sel):
-        if r not in rmap:
-            rmap[r] = len(rnames)
-            rnames.append(r)
-        ridx[j] = rmap[r]
+    rel_sel = rel[sel]
+    if len(rel_sel) and (rel_sel < 0).any():
+        raise KeyError("label")
+    tidx, tcode_of = _first_appearance(tcodes)
+    tvals = P["tvals"]
+    tnames = [tvals[c] for c in tcode_of.tolist()]
+    ridx, rcode_of = _first_appearance(rel_sel)
+    rnames = [P["rnames"][c] for c in rcode_of.tolist()]
     g = Graph(tidx, [str(t) if not isinstance(t, str) else t for t in tnames],
               src[sel].astype(np.int32), dst[sel].astype(np.int32), ridx, rnames,
               node_ids=node_ids, labels=labels)

@@ -391,6 +391,28 @@ int dps_write_topk_log(const char* path, int append, int64_t row_begin, int64_t 
                        const char* label_blob, const int64_t* label_off, double stage_seconds,
                        double overall_seconds, int n_threads);
 
+/* ---------------------------------------------------------------------------
+ * f1. Native GEXF scan for read_dblp_nx_file (DPathSim_APVPA.py:114-129, the
+ * networkx.read_gexf of :116), host-only.  dps_gexf_open mmaps and scans the
+ * file; *status 0 = parsed, 1 = outside the supported subset (nested <nodes>,
+ * DOCTYPE, numeric attribute types, undefined attvalue keys, edge-type
+ * conflicts, I/O errors): the caller runs its own parser, which reports the
+ * reference's exceptions.  dps_gexf_info: 0 nodes, 1 edges, 2 type names,
+ * 3 relationship names, 4 directed, 5-8 bytes of node ids / labels / type
+ * names / relationship names, 9 bytes of the edge-id buffer.  dps_gexf_export
+ * fills caller arrays: string tables as concatenated UTF-8 + int64 offsets
+ * [n+1]; lab_null[i] = 1 when the node has no label; ntype / e_rel = -1 when
+ * absent (node without node_type, edge without relationship); e_key_off[j] =
+ * offset of edge j's NUL-terminated id in key_buf, -1 when it has none.
+ * ------------------------------------------------------------------------- */
+void* dps_gexf_open(const char* path, int32_t* status);
+int64_t dps_gexf_info(void* h, int32_t what);
+int dps_gexf_export(void* h, int64_t* id_off, char* id_buf, int64_t* lab_off, char* lab_buf,
+                    uint8_t* lab_null, int32_t* ntype, int64_t* type_off, char* type_buf,
+                    int32_t* e_src, int32_t* e_dst, int32_t* e_rel, int64_t* e_key_off,
+                    char* key_buf, int64_t* rel_off, char* rel_buf);
+void dps_gexf_close(void* h);
+
 #ifdef __cplusplus
 }
 #endif
