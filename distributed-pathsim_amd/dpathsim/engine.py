@@ -7,6 +7,7 @@ queries of DPathSim_APVPA.py:70-109 (see include/dpathsim.h per entry point).
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -187,8 +188,9 @@ class PathSimEngine:
             # A3: SpGEMM C = W_AP . W_PX over EVERY AP row (author rows [0, NA)
             # first, then untyped author_of sources), capacities from the
             # raw-edge bounds (sum_c >= nnz C), no size read-back.  Papers with
-            # at most one mid (APVPA): gather + segmented unique; otherwise the
-            # hash SpGEMM.
+            # at most one mid (APVPA): gather + segmented unique; otherwise
+            # expand + segmented sort/unique (config4: 3.2 ms against 9.8 ms for
+            # the hash SpGEMM, kept behind DPATHSIM_SPGEMM=hash).
             cap = bnd.sum_c
             c_ptr, c_nnz = self._empty(NR + 1, torch.int64), self._empty(2, torch.int64)
             sp_status = self._empty(1, torch.int32)
@@ -202,6 +204,15 @@ class PathSimEngine:
                               _ptr(c_val) if numeric else None, _ptr(c_nnz), _ptr(sws),
                               sws.numel(), st)
                 del vp
+            elif os.environ.get("DPATHSIM_SPGEMM", "sort") == "sort":
+                # expand + segmented sort/unique (sum_c bounds the expansion)
+                sws = self._ws(_lib.size("dps_spgemm_workspace_size", NR, bnd.sum_c))
+                sp_status.zero_()
+                for numeric in (False, True):
+                    _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, NR, _ptr(px_ptr),
+                              _ptr(px_col), NP, _ptr(c_ptr), _ptr(c_col) if numeric else None,
+                              _ptr(c_val) if numeric else None, _ptr(c_nnz), bnd.sum_c, _ptr(sws),
+                              sws.numel(), st)
             else:
                 sws = self._ws(_lib.size("dps_spgemm_hash_workspace_size", NR, bnd.max_row_expand))
                 for numeric in (False, True):

@@ -153,12 +153,14 @@ def test_topk_rows_matches_contiguous_launch():
     assert all(a.shape[0] == 0 for a in eng.topk_rows(10, np.zeros(0, np.int64)))
 
 
-@pytest.mark.parametrize("multi", [1, 3])
-def test_spgemm_long_and_huge_rows(multi):
-    """The hash SpGEMM's three row paths: lane (L <= 16), LDS hash (16 < L <=
-    4096) and global-scratch sort (L > 4096), with papers of 1 or up to 3
-    venues each (repeats dropped by the PX distinct) -- C, g and the top-k
-    against the oracle."""
+@pytest.mark.parametrize("multi,spgemm", [(1, "sort"), (3, "sort"), (3, "hash")])
+def test_spgemm_long_and_huge_rows(multi, spgemm, monkeypatch):
+    """Rows of every length class, papers of 1 (single-mid path) or up to 3
+    venues each (repeats dropped by the PX distinct), through the multi-mid
+    SpGEMMs: expand + segmented sort/unique (the default) and the hash SpGEMM
+    (lane L <= 16, LDS hash 16 < L <= 4096, global-scratch sort L > 4096) --
+    C, g and the top-k against the oracle."""
+    monkeypatch.setenv("DPATHSIM_SPGEMM", spgemm)
     import pathsim_oracle as po
     from dpathsim.engine import build_engine
     from dpathsim.graph import Graph
