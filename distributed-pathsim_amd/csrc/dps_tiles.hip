@@ -193,7 +193,8 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restri
 }
 
 // --------------------------------------------------------------------------
-// Block-local tile build (n_mids <= kBlkMids): a block owns a contiguous range
+// Block-local tile build (kBlkMids mids per block; more mids take one block per
+// mid range, MidRange below): a block owns a contiguous range
 // of kBlkLabels target labels -- all inside one tile -- and counts its entries
 // per venue in LDS, so the hot buckets of heavy venues take one global atomic
 // per block instead of one per entry.  The scatter pass reserves each venue's
@@ -428,6 +429,22 @@ __device__ __forceinline__ SubRange sub_range(uint32_t n, uint32_t sb, int S) {
   return r;
 }
 
+// Mid range r of the block-local build: mids [m0, m0 + n), n <= kBlkMids (the
+// LDS counters of one block); a build over more mids launches one block per
+// (part, sub-block, range), each walking the part's entries and keeping its
+// range's.
+struct MidRange {
+  int64_t m0;
+  int n;
+};
+__device__ __forceinline__ MidRange mid_range(int64_t r, int64_t n_mids) {
+  MidRange m;
+  m.m0 = r * kBlkMids;
+  const int64_t left = n_mids - m.m0;
+  m.n = static_cast<int>(left < kBlkMids ? (left > 0 ? left : 0) : kBlkMids);
+  return m;
+}
+
 // Part p = (t, h) of tile t (labels_per_block labels, P parts per tile),
 // sub-block sb of up to S (sub_range: one per kSubEntries entries of the part).
 // Counting writes the sub-block's per-venue piece counts and maxima into the
@@ -439,7 +456,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
     const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
     const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm,
     const int64_t* __restrict__ g, int64_t n_targets, int64_t n_mids, int shift, int64_t T,
-    int labels_per_block, int P, int S, const uint32_t* __restrict__ part_n,
+    int labels_per_block, int P, int S, int n_ranges, const uint32_t* __restrict__ part_n,
     uint32_t* __restrict__ cntp, uint32_t* __restrict__ mxp,
     unsigned long long* __restrict__ gmin, int32_t* __restrict__ status) {
   __shared__ uint32_t cnt_s[kBlkMids];
@@ -450,14 +467,16 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
   __shared__ uint32_t wsum[kBlkThreads / kWave];
   __shared__ unsigned long long gmin_s;
   __shared__ int ovf_s;
-  // sub-block major (block = sb * n_parts + part): the parts' first sub-blocks
-  // -- the only ones most parts use -- spread over every XCD
-  const int64_t n_parts = gridDim.x / S;
+  // sub-block major (block = (range * S + sb) * n_parts + part): the parts'
+  // first sub-blocks -- the only ones most parts use -- spread over every XCD
+  const int64_t n_parts = gridDim.x / (static_cast<int64_t>(S) * n_ranges);
   const int64_t part = blockIdx.x % n_parts;
-  const uint32_t sb = static_cast<uint32_t>(blockIdx.x / n_parts);
+  const int64_t q = blockIdx.x / n_parts;
+  const uint32_t sb = static_cast<uint32_t>(q % S);
+  const MidRange mr = mid_range(q / S, n_mids);
   const SubRange sr = sub_range(part_n[part], sb, S);
   if (static_cast<int>(sb) >= sr.n_sub) return;   // block-uniform: before any barrier
-  for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) { cnt_s[v] = 0; mx_s[v] = 0; }
+  for (int v = threadIdx.x; v < mr.n; v += kBlkThreads) { cnt_s[v] = 0; mx_s[v] = 0; }
   if (threadIdx.x == 0) { gmin_s = ~0ull; ovf_s = 0; }
   const bool p16 = shift <= kP16MaxShift;
   const int64_t l0 = part * labels_per_block;
@@ -467,27 +486,30 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
   __syncthreads();
   const BlockRows R{rel_s, d_s};
   const int nl = static_cast<int>(l1 - l0);
-  const bool do_g = gmin && sb == 0;
+  const bool do_g = gmin && sb == 0 && mr.m0 == 0;
   [[maybe_unused]] const uint32_t n = stage_rows(c_ptr, perm, do_g ? g : nullptr, l0, l1, R, wsum, &gmin_s);
   DPS_DASSERT(n == part_n[part]);
   if (sr.e1 - sr.e0 <= kMaxStrips * kWave) strip_table(R, nl, sr.e0, sr.e1, tab_s);
   const uint32_t lab0 = static_cast<uint32_t>(l0);
   walk_strips(R, nl, sr.e0, sr.e1, tab_s, c_col, c_val, [&](int i, int32_t v, int32_t c) {
     if (c > 0xFFFF) ovf_s = 1;
-    atomicAdd(&cnt_s[v], n_pieces(p16, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
-    atomicMax(&mx_s[v], static_cast<uint32_t>(c));
+    const uint32_t lv = static_cast<uint32_t>(v - mr.m0);
+    if (lv >= static_cast<uint32_t>(mr.n)) return;   // another block's mid range
+    atomicAdd(&cnt_s[lv], n_pieces(p16, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
+    atomicMax(&mx_s[lv], static_cast<uint32_t>(c));
   });
   __syncthreads();
   if (threadIdx.x == 0 && ovf_s && status) *status = DPS_ERR_OVERFLOW;
-  for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) {
-    if (!cnt_s[v]) continue;
+  for (int lv = threadIdx.x; lv < mr.n; lv += kBlkThreads) {
+    if (!cnt_s[lv]) continue;
+    const int64_t v = mr.m0 + lv;
     const int64_t slot = (v * T + t) * P + h;
     if (sr.n_sub == 1) {
-      cntp[slot] = cnt_s[v];
-      mxp[slot] = mx_s[v];
+      cntp[slot] = cnt_s[lv];
+      mxp[slot] = mx_s[lv];
     } else {
-      atomicAdd(&cntp[slot], cnt_s[v]);
-      atomicMax(&mxp[slot], mx_s[v]);
+      atomicAdd(&cntp[slot], cnt_s[lv]);
+      atomicMax(&mxp[slot], mx_s[lv]);
     }
   }
   if (threadIdx.x == 0 && do_g && gmin_s != ~0ull) atomicMin(&gmin[t], gmin_s);
@@ -520,7 +542,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_parts_fix(uint32_t* __restrict_
 __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
     const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
     const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm, int64_t n_targets,
-    int64_t n_mids, int shift, int64_t T, int labels_per_block, int P, int S,
+    int64_t n_mids, int shift, int64_t T, int labels_per_block, int P, int S, int n_ranges,
     const uint32_t* __restrict__ part_n, const int64_t* __restrict__ offp,
     uint32_t* __restrict__ curp, uint32_t* __restrict__ ent) {
   __shared__ uint32_t cnt_s[kBlkMids];
@@ -529,14 +551,15 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
   __shared__ int64_t d_s[kBlkLabels];
   __shared__ int tab_s[kMaxStrips + 1];
   __shared__ uint32_t wsum[kBlkThreads / kWave];
-  // sub-block major (block = sb * n_parts + part): the parts' first sub-blocks
-  // -- the only ones most parts use -- spread over every XCD
-  const int64_t n_parts = gridDim.x / S;
+  // block = (range * S + sb) * n_parts + part, as in k_tile_count_blk
+  const int64_t n_parts = gridDim.x / (static_cast<int64_t>(S) * n_ranges);
   const int64_t part = blockIdx.x % n_parts;
-  const uint32_t sb = static_cast<uint32_t>(blockIdx.x / n_parts);
+  const int64_t q = blockIdx.x / n_parts;
+  const uint32_t sb = static_cast<uint32_t>(q % S);
+  const MidRange mr = mid_range(q / S, n_mids);
   const SubRange sr = sub_range(part_n[part], sb, S);
   if (static_cast<int>(sb) >= sr.n_sub) return;   // block-uniform: before any barrier
-  for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) cnt_s[v] = 0;
+  for (int v = threadIdx.x; v < mr.n; v += kBlkThreads) cnt_s[v] = 0;
   const bool p16 = shift <= kP16MaxShift;
   const int64_t l0 = part * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
@@ -550,25 +573,29 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
   if (sr.e1 - sr.e0 <= kMaxStrips * kWave) strip_table(R, nl, sr.e0, sr.e1, tab_s);
   const uint32_t lab0 = static_cast<uint32_t>(l0) & ymask;
   if (sr.n_sub == 1) {
-    for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads)
-      base_s[v] = static_cast<unsigned long long>(offp[(v * T + t) * P + h]);
+    for (int lv = threadIdx.x; lv < mr.n; lv += kBlkThreads)
+      base_s[lv] = static_cast<unsigned long long>(offp[((mr.m0 + lv) * T + t) * P + h]);
   } else {
     walk_strips(R, nl, sr.e0, sr.e1, tab_s, c_col, c_val, [&](int i, int32_t v, int32_t c) {
-      atomicAdd(&cnt_s[v], n_pieces(p16, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
+      const uint32_t lv = static_cast<uint32_t>(v - mr.m0);
+      if (lv >= static_cast<uint32_t>(mr.n)) return;
+      atomicAdd(&cnt_s[lv], n_pieces(p16, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
     });
     __syncthreads();
-    for (int64_t v = threadIdx.x; v < n_mids; v += kBlkThreads) {
-      const uint32_t nv = cnt_s[v];
+    for (int lv = threadIdx.x; lv < mr.n; lv += kBlkThreads) {
+      const uint32_t nv = cnt_s[lv];
       if (!nv) continue;
-      const int64_t slot = (v * T + t) * P + h;
-      base_s[v] = static_cast<unsigned long long>(offp[slot] + atomicAdd(&curp[slot], nv));
+      const int64_t slot = ((mr.m0 + lv) * T + t) * P + h;
+      base_s[lv] = static_cast<unsigned long long>(offp[slot] + atomicAdd(&curp[slot], nv));
     }
   }
   __syncthreads();
   walk_strips(R, nl, sr.e0, sr.e1, tab_s, c_col, c_val, [&](int i, int32_t v, int32_t c) {
+    const uint32_t lv = static_cast<uint32_t>(v - mr.m0);
+    if (lv >= static_cast<uint32_t>(mr.n)) return;
     const uint32_t lab = lab0 + static_cast<uint32_t>(i);
     const unsigned long long pos =
-        atomicAdd(&base_s[v], static_cast<unsigned long long>(
+        atomicAdd(&base_s[lv], static_cast<unsigned long long>(
                                   n_pieces(p16, static_cast<uint32_t>(c), lab)));
     put_entry(p16, ent, static_cast<int64_t>(pos), static_cast<uint32_t>(c), lab);
   });
@@ -684,9 +711,21 @@ int tile_sub() {
   return sub < 1 || sub > 64 ? kBlkSub : sub;
 }
 
+// Builds over more than kBlkMids mids: the block-local path with one block
+// per mid range reads C once per range, so it is taken up to kMaxMidRanges
+// ranges (config5, 20k venues, 3 ranges: 7.1 -> 2.8 ms) and the global-atomic
+// counting sort above (config4, 200k topics, 25 ranges: 7.5 vs 13.7 ms);
+// DPATHSIM_TILE_GLOBAL=1 / 0 forces one or the other.
+constexpr int64_t kMaxMidRanges = 8;
+bool tile_global(int64_t n_mids) {
+  if (n_mids <= kBlkMids) return false;
+  if (const char* e = std::getenv("DPATHSIM_TILE_GLOBAL")) return std::atoi(e) != 0;
+  return (n_mids + kBlkMids - 1) / kBlkMids > kMaxMidRanges;
+}
+
 // Parts per tile of the block-local build (1 on the global-atomic path).
 int64_t tile_parts(int64_t n_mids, int32_t tile_w) {
-  if (n_mids > kBlkMids) return 1;
+  if (tile_global(n_mids)) return 1;
   const int lpb = tile_lpb(tile_w);
   return tile_w > lpb ? tile_w / lpb : 1;
 }
@@ -770,7 +809,9 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   auto st = static_cast<hipStream_t>(stream);
   const int64_t T = (n_targets + tile_w - 1) / tile_w;
   const int64_t nb = n_mids * T;
-  const bool blk = n_mids <= kBlkMids;   // block-local LDS counting, parts per tile
+  // block-local LDS counting, parts per tile, one block per kBlkMids mids
+  const bool blk = !tile_global(n_mids);
+  const int n_ranges = static_cast<int>(n_mids > 0 ? (n_mids + kBlkMids - 1) / kBlkMids : 1);
   const int P = static_cast<int>(tile_parts(n_mids, tile_w));
   const int64_t np = nb * P;
   Carve c(ws, ws_bytes);
@@ -788,7 +829,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   const int lpb = tile_lpb(tile_w);
   const int64_t nblk = (n_targets + lpb - 1) / lpb;
   const int S = tile_sub();
-  DPS_REQUIRE(nblk * S < INT32_MAX, DPS_ERR_OVERFLOW, "too many tile-build blocks");
+  DPS_REQUIRE(nblk * S * n_ranges < INT32_MAX, DPS_ERR_OVERFLOW, "too many tile-build blocks");
   const bool p16 = shift <= kP16MaxShift;   // counts and offsets are in entries
   const uint32_t per16 = p16 ? 8u : 4u;
   const bool fused_parts = blk && n_targets > 0 && nblk <= kPartLds;
@@ -818,10 +859,10 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     }
     if (tile_maxc) DPS_HIP_RET(hipMemsetAsync(tile_maxc + nb, 0, sizeof(uint32_t), st));
     if (n_targets > 0 && nb > 0) {
-      k_tile_count_blk<<<static_cast<unsigned>(nblk * S), kBlkThreads, 0, st>>>(
+      k_tile_count_blk<<<static_cast<unsigned>(nblk * S * n_ranges), kBlkThreads, 0, st>>>(
           c_ptr, c_col, c_val, perm_or_null, tile_gmin ? g : nullptr, n_targets, n_mids, shift, T,
-          lpb, P, S, part_n, cntp, mxp, reinterpret_cast<unsigned long long*>(tile_gmin),
-          status_dev);
+          lpb, P, S, n_ranges, part_n, cntp, mxp,
+          reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
       DPS_LAUNCHED();
     }
     if (nb > 0) {
@@ -833,9 +874,9 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, P, nb, p16 ? 1 : 0, tile_off);
     DPS_LAUNCHED();
     if (n_targets > 0 && nb > 0) {
-      k_tile_scatter_blk<<<static_cast<unsigned>(nblk * S), kBlkThreads, 0, st>>>(
-          c_ptr, c_col, c_val, perm_or_null, n_targets, n_mids, shift, T, lpb, P, S, part_n, off64,
-          curp, tile_ent);
+      k_tile_scatter_blk<<<static_cast<unsigned>(nblk * S * n_ranges), kBlkThreads, 0, st>>>(
+          c_ptr, c_col, c_val, perm_or_null, n_targets, n_mids, shift, T, lpb, P, S, n_ranges,
+          part_n, off64, curp, tile_ent);
       DPS_LAUNCHED();
     }
     if (nb > 0) {

@@ -82,6 +82,19 @@ def test_aptpa_multi_topic():
     _check(build_engine(t, tile_w=1024), _oracle(t), 10)
 
 
+@pytest.mark.parametrize("tile_w,glob", [(256, "0"), (1024, "0"), (8192, "0"), (8192, "1")])
+def test_many_mids_tile_build(tile_w, glob, monkeypatch):
+    """More mids than one block's LDS counters (20,000 venues > 8192): the
+    block-local tile build with one block per mid range (default) and the
+    global-atomic build (DPATHSIM_TILE_GLOBAL=1) against the oracle."""
+    monkeypatch.setenv("DPATHSIM_TILE_GLOBAL", glob)
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_dblp
+    t = synth_dblp(6_000, 24_000, 20_000, seed=29).typed()
+    assert t.n_mids > 2 * 8192
+    _check(build_engine(t, tile_w=tile_w), _oracle(t), 10)
+
+
 @pytest.mark.parametrize("tile_w", [16384, 32768])
 def test_config3_sample_rows(tile_w):
     """Full-size config3 (1M authors): two 1500-row slices vs the C oracle."""
