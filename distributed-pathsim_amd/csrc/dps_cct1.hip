@@ -412,8 +412,13 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
   return chunks;
 }
 
+// Top-k lists up to DPS_W5_KPL * 64 slots run 5 waves per SIMD (96 VGPRs),
+// longer ones 4 (128 VGPRs).
+#ifndef DPS_W5_KPL
+#define DPS_W5_KPL 1
+#endif
 template <int KPL>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL == 1 ? 5 : 4))) void k_cct1(CctParams p) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DPS_W5_KPL ? 5 : 4))) void k_cct1(CctParams p) {
   // LDS: the accumulator at address 0 (scatter ORs the in-tile offset into 0)
   // then the candidate queue.
   __shared__ __attribute__((aligned(16))) uint32_t lds[kAcc1];
@@ -592,7 +597,7 @@ int launch1(const CctParams& p, hipStream_t st) {
   int dev = 0, n_cu = 256;
   DPS_HIP_RET(hipGetDevice(&dev));
   DPS_HIP_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-  int wpc = KPL == 1 ? 20 : 16;   // 5 (k <= 64) or 4 waves per SIMD, 8 KB of LDS each
+  int wpc = KPL <= DPS_W5_KPL ? 20 : 16;   // 5 or 4 waves per SIMD, 8 KB of LDS each
   if (const char* e = std::getenv("DPATHSIM_LEAN_WPC")) wpc = std::atoi(e);   // experiments
   if (wpc < 1 || wpc > 20) wpc = 20;
   int64_t grid = static_cast<int64_t>(n_cu) * wpc;
