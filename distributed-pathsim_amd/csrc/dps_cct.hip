@@ -512,14 +512,85 @@ int dispatch(const CctParams& p, int nw, int k, hipStream_t st) {
   return launch<4, 4, P16>(p, st);
 }
 
+// ---- heavy-first dequeue list (dps_heavy_first) ---------------------------
+// Descending key of a row's work on a log scale, four steps per octave: one
+// 8-bit radix pass orders the rows heaviest first (stable: equal keys keep the
+// row order) -- the hot kernel's dequeue order is a load-balance heuristic
+// and any order gives identical results.
+__global__ __launch_bounds__(256) void k_work_key(const int64_t* __restrict__ work, int64_t n,
+                                                  uint64_t* __restrict__ key) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t w = work[i];
+    uint32_t b = 0;
+    if (w > 0) {
+      const uint64_t u = static_cast<uint64_t>(w);
+      const int e = 63 - __clzll(static_cast<long long>(u));
+      const uint32_t frac = static_cast<uint32_t>((u << (63 - e)) >> 61) & 3u;   // 2 bits below the top one
+      b = 1u + 4u * static_cast<uint32_t>(e) + frac;                                 // <= 252
+    }
+    key[i] = 255u - b;
+  }
+}
+
+// dq = the sorted rows (+ row_begin), the first n_split of them repeated
+// `pieces` times in front (their piece slots), then the rest.
+__global__ __launch_bounds__(256) void k_dequeue_list(const uint32_t* __restrict__ sorted, int64_t n,
+                                                      int64_t row_begin, int64_t n_split,
+                                                      int pieces, int32_t* __restrict__ dq) {
+  const int64_t n_out = n + n_split * (pieces - 1);
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n_out;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t src = i < n_split * pieces ? i / pieces : i - n_split * (pieces - 1);
+    dq[i] = static_cast<int32_t>(row_begin + sorted[src]);
+  }
+}
+
 }  // namespace
 }  // namespace dps
+
 
 using namespace dps;
 
 extern "C" {
 
 size_t dps_cct_topk_workspace_size(void) { return 256; }
+
+size_t dps_heavy_first_workspace_size(int64_t n_rows) {
+  const size_t m = static_cast<size_t>(n_rows > 0 ? n_rows : 1);
+  return 2 * align_up(m * sizeof(uint64_t)) + align_up(m * sizeof(uint32_t)) +
+         align_up(radix_sort_workspace_size(n_rows)) + 1024;
+}
+
+int dps_heavy_first(const int64_t* work, int64_t n_rows, int64_t row_begin, int64_t n_split,
+                    int32_t pieces, int32_t* dq, void* ws, size_t ws_bytes, void* stream) {
+  DPS_REQUIRE(n_rows >= 0 && n_split >= 0 && n_split <= n_rows, DPS_ERR_INVALID,
+              "need 0 <= n_split <= n_rows");
+  DPS_REQUIRE(pieces >= 1 && pieces <= 64, DPS_ERR_INVALID, "pieces must be in [1, 64]");
+  DPS_REQUIRE(row_begin >= 0 && row_begin + n_rows <= INT32_MAX, DPS_ERR_OVERFLOW,
+              "row indices exceed int32");
+  DPS_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 256 == 0, DPS_ERR_WORKSPACE,
+              "workspace not 256-byte aligned");
+  DPS_REQUIRE(ws_bytes >= dps_heavy_first_workspace_size(n_rows), DPS_ERR_WORKSPACE,
+              "heavy_first workspace too small");
+  if (n_rows == 0) return DPS_OK;
+  DPS_REQUIRE(work && dq, DPS_ERR_INVALID, "null work / dq");
+  auto st = static_cast<hipStream_t>(stream);
+  Carve c(ws, ws_bytes);
+  uint64_t* key = c.take<uint64_t>(n_rows);
+  uint64_t* key_sorted = c.take<uint64_t>(n_rows);
+  uint32_t* rows = c.take<uint32_t>(n_rows);
+  const size_t rws_bytes = radix_sort_workspace_size(n_rows);
+  void* rws = c.take<char>(rws_bytes);
+  DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "heavy_first workspace carve failed");
+  k_work_key<<<grid_for(n_rows, 256), 256, 0, st>>>(work, n_rows, key);
+  DPS_LAUNCHED();
+  DPS_HIP_RET(radix_sort_pairs(key, nullptr, key_sorted, rows, n_rows, 8, rws, rws_bytes, st));
+  const int64_t n_out = n_rows + n_split * (pieces - 1);
+  k_dequeue_list<<<grid_for(n_out, 256), 256, 0, st>>>(rows, n_rows, row_begin, n_split, pieces, dq);
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
 
 static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
                          const int64_t* g, const int64_t* g_t, const int32_t* t_perm,

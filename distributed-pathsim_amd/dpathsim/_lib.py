@@ -76,6 +76,8 @@ SIGNATURES = {
                                      _p, _i64, _i64, _p, _i64, _p, _p, _i64, _p, _p, _p, _i32, _p,
                                      _p, _p, _p, _sz, _p]),
     "dps_topk_merge": (C.c_int, [_p, _p, _p, _p, _i64, _i32, _i32, _i64, _i64, _p, _p, _p, _p]),
+    "dps_heavy_first_workspace_size": (_sz, [_i64]),
+    "dps_heavy_first": (C.c_int, [_p, _i64, _i64, _i64, _i32, _p, _p, _sz, _p]),
     "dps_walk_row": (C.c_int, [_p, _p, _i64, _p, _i64, _i64, _i32, _p, _p, _p, _p]),
     "dps_row_scores": (C.c_int, [_p, _p, _i64, _i64, _p, _p, _p]),
     "dps_pair_count": (C.c_int, [_p, _p, _i64, _p, _p, _i64, _p, _p]),

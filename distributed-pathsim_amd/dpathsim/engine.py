@@ -91,6 +91,7 @@ class PathSimEngine:
         self.built = False
         self.checked = False
         self._dev = {}
+        self._piece_cache = {}
 
     # ------------------------------------------------------------------ utils
     @property
@@ -370,21 +371,27 @@ class PathSimEngine:
                   self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
                   _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]))
         with torch.cuda.device(self.device):
-            order = None
+            dq = None
             if heavy_first and R > 1:
-                w = self.row_work()[row_begin:row_end]
-                order = (torch.argsort(w, descending=True, stable=True) + row_begin).to(torch.int32)
+                # rows heaviest first by their C^T entry count (log scale, one
+                # radix pass), the M heaviest as M*P pieces in front
+                dq = torch.empty(R + M * (P - 1), dtype=torch.int32, device=self.device)
+                hws = self._ws(_lib.size("dps_heavy_first_workspace_size", R))
+                _lib.call("dps_heavy_first", _ptr(d["row_terms"][row_begin:row_end]), R,
+                          int(row_begin), M, P if M else 1, _ptr(dq), _ptr(hws), hws.numel(),
+                          self.stream)
             if M == 0:
-                _lib.call("dps_cct_topk", *common, int(row_begin), int(row_end), _ptr(order),
+                _lib.call("dps_cct_topk", *common, int(row_begin), int(row_end), _ptr(dq),
                           int(k), _ptr(idx), _ptr(cnt), _ptr(sc), _ptr(d["topk_ws"]),
                           d["topk_ws"].numel(), self.stream)
                 return idx, cnt, sc
-            # M heaviest rows -> M*P pieces first in the dequeue list, then the rest
-            heavy = order[:M]
-            part = torch.arange(P + 1, device=self.device, dtype=torch.int64) * T // P
-            t0 = part[:-1].to(torch.int32).repeat(M)
-            t1 = part[1:].to(torch.int32).repeat(M)
-            dq = torch.cat([heavy.repeat_interleave(P), order[M:]])
+            # piece tile ranges: the same for every split row (cached)
+            key = ("pieces", M, P, T)
+            if key not in self._piece_cache:
+                part = torch.arange(P + 1, device=self.device, dtype=torch.int64) * T // P
+                self._piece_cache = {key: (part[:-1].to(torch.int32).repeat(M),
+                                           part[1:].to(torch.int32).repeat(M))}
+            t0, t1 = self._piece_cache[key]
             n_p = M * P
             pbuf = (torch.empty((n_p, k), dtype=torch.int32, device=self.device),
                     torch.empty((n_p, k), dtype=torch.int64, device=self.device),

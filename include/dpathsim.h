@@ -343,6 +343,16 @@ int dps_topk_merge(const int32_t* piece_idx, const int64_t* piece_cnt, const dou
                    int64_t n_targets, int64_t row_begin, int32_t* out_idx, int64_t* out_cnt,
                    double* out_score, void* stream);
 
+/* Heavy-first dequeue list for dps_cct_topk / dps_cct_topk_split (no
+ * counterpart in the reference; load balance of the all-pairs loop :36):
+ * rows row_begin + [0, n_rows) ordered by work[i] descending on a log scale
+ * (four steps per octave, equal steps in row order), the first n_split of them
+ * repeated `pieces` times in front -- dq has n_rows + n_split * (pieces - 1)
+ * entries.  Any order gives identical top-k results. */
+size_t dps_heavy_first_workspace_size(int64_t n_rows);
+int dps_heavy_first(const int64_t* work, int64_t n_rows, int64_t row_begin, int64_t n_split,
+                    int32_t pieces, int32_t* dq, void* ws, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Single-source row (the reference's run() loop, :30-50): for one sparse C row
  * (src_col/src_val, src_len entries, device), the dense pairwise walk
