@@ -150,15 +150,17 @@ def rescore(packed: torch.Tensor, den: torch.Tensor, row_begin: int = 0):
 
 
 def gather_topk_compact(parts, den: torch.Tensor, n_rows: int, world: int, group=None,
-                        out=None, bounds=None, dst: int = 0):
+                        out=None, bounds=None, dst: int = 0, force_collective: bool = False):
     """As :func:`gather_topk`, with 8 B per slot on the wire: every rank sends
     (count << 32) | index words; rank ``dst`` rebuilds the scores from its own
     copy of the denominator term ``den`` (every rank holds all of g).  ``parts``:
-    (idx, cnt[, score]) [max_shard, k] or packed int64 [max_shard, k]."""
+    (idx, cnt[, score]) [max_shard, k] or packed int64 [max_shard, k].
+    ``force_collective`` runs the gather even for one rank (lets a one-GPU box
+    exercise the RCCL call)."""
     if bounds is None:
         bounds = [shard_bounds(n_rows, r, world) for r in range(world)]
     packed = parts if isinstance(parts, torch.Tensor) else pack_counts(parts[0], parts[1])
-    if world == 1:
+    if world == 1 and not force_collective:
         return rescore(packed[:bounds[0][1] - bounds[0][0]], den)
     m = max_shard(n_rows, world, bounds)
     if packed.shape[0] != m:

@@ -178,3 +178,39 @@ def test_gloo_two_ranks_engine_shards(tmp_path):
     mp.start_processes(_engine_worker, args=(2, _free_port(), 10, str(out)), nprocs=2,
                        join=True, start_method="spawn")
     assert out.read_text() == "ok"
+
+
+def _rccl_worker(rank, world, port, k, result_path):
+    """The compact gather on the nccl (RCCL) backend with one rank: the same
+    dist.gather call bench.py makes at N > 1 (a one-GPU box cannot host two
+    RCCL ranks)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    try:
+        import pathsim_oracle as po
+        from dpathsim.dist import pack_counts
+        from dpathsim.engine import build_engine
+        from dpathsim.synth import synth_dblp
+        t = synth_dblp(4000, 12000, 200, seed=8).typed()
+        eng = build_engine(t, device="cuda:0")
+        na = t.n_authors
+        idx, cnt, _ = eng.topk(k)
+        out = torch.empty((na, k), dtype=torch.int64, device="cuda:0")
+        gi, gc, gs = gather_topk_compact(pack_counts(idx, cnt), eng.tensor("den")[:na], na, 1,
+                                         out=out, force_collective=True)
+        fi, fc, fs = po.COracle.from_typed(t).topk(k, 0, na)
+        ok = (np.array_equal(gi.cpu().numpy(), fi) and np.array_equal(gc.cpu().numpy(), fc)
+              and np.array_equal(gs.cpu().numpy().view(np.int64), fs.view(np.int64)))
+        with open(result_path, "w") as f:
+            f.write("ok" if ok else "mismatch")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_compact_gather_one_rank(tmp_path):
+    out = tmp_path / "result.txt"
+    mp.start_processes(_rccl_worker, args=(1, _free_port(), 10, str(out)), nprocs=1,
+                       join=True, start_method="spawn")
+    assert out.read_text() == "ok"
