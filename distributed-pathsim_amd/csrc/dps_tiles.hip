@@ -111,7 +111,9 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
       const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
       atomicAdd(&cnt[b], n_pieces(shift <= kP16MaxShift, static_cast<uint32_t>(c),
                                   static_cast<uint32_t>(label_of(rank, y))));
-      if (maxc) atomicMax(&maxc[b], static_cast<uint32_t>(c));
+      // C = 1 (most entries when buckets are sparse) needs no atomic: k_round4
+      // raises the maximum of every non-empty bucket to at least 1
+      if (maxc && c > 1) atomicMax(&maxc[b], static_cast<uint32_t>(c));
     }
   }
   __syncthreads();
@@ -123,10 +125,13 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
 // Buckets are padded to 16 B (4 uint32 or 8 uint16 entries) so the hot
 // kernel's 16-byte chunks never straddle two buckets; padding entries have C = 0.
 __global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, int64_t n,
-                                                   uint32_t per16) {
+                                                   uint32_t per16, uint32_t* __restrict__ maxc) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
-       i += static_cast<int64_t>(gridDim.x) * kBlock)
-    cnt[i] = padded_count(cnt[i], per16);
+       i += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const uint32_t c = cnt[i];
+    cnt[i] = padded_count(c, per16);
+    if (maxc && c > 0 && maxc[i] == 0) maxc[i] = 1;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__ off, int P,
@@ -897,7 +902,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     DPS_LAUNCHED();
   }
   if (nb > 0) {
-    k_round4<<<grid_for(nb, kBlock), kBlock, 0, st>>>(cnt, nb, per16);
+    k_round4<<<grid_for(nb, kBlock), kBlock, 0, st>>>(cnt, nb, per16, tile_maxc);
     DPS_LAUNCHED();
   }
   DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, off64, nb, sws, scan_ws, st));
