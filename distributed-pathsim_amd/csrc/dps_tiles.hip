@@ -501,7 +501,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
     const uint32_t lv = static_cast<uint32_t>(v - mr.m0);
     if (lv >= static_cast<uint32_t>(mr.n)) return;   // another block's mid range
     atomicAdd(&cnt_s[lv], n_pieces(p16, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
-    atomicMax(&mx_s[lv], static_cast<uint32_t>(c));
+    if (c > 1) atomicMax(&mx_s[lv], static_cast<uint32_t>(c));   // 1 by k_tile_parts_fix
   });
   __syncthreads();
   if (threadIdx.x == 0 && ovf_s && status) *status = DPS_ERR_OVERFLOW;
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
       mxp[slot] = mx_s[lv];
     } else {
       atomicAdd(&cntp[slot], cnt_s[lv]);
-      atomicMax(&mxp[slot], mx_s[lv]);
+      if (mx_s[lv]) atomicMax(&mxp[slot], mx_s[lv]);
     }
   }
   if (threadIdx.x == 0 && do_g && gmin_s != ~0ull) atomicMin(&gmin[t], gmin_s);
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_parts_fix(uint32_t* __restrict_
     }
     cnt[b] = tot;
     cntp[b * P + P - 1] += padded_count(tot, per16) - tot;
-    if (maxc) maxc[b] = mx;
+    if (maxc) maxc[b] = (tot > 0 && mx == 0) ? 1u : mx;   // C = 1 entries skip the max
   }
 }
 
