@@ -122,6 +122,24 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
       if (gmin_s[i] != ~0ull) atomicMin(&gmin[i], gmin_s[i]);
 }
 
+// Up to eight dword ranges set to a value in one launch (the block-local build's
+// counters, status and tile minima: one kernel instead of a fill per array).
+struct FillSet {
+  uint32_t* p[8];
+  int64_t n[8];
+  uint32_t v[8];
+  int k;
+};
+__global__ __launch_bounds__(kBlock) void k_fill_set(FillSet s) {
+  for (int r = 0; r < s.k; ++r) {
+    uint32_t* __restrict__ p = s.p[r];
+    const uint32_t v = s.v[r];
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < s.n[r];
+         i += static_cast<int64_t>(gridDim.x) * kBlock)
+      p[i] = v;
+  }
+}
+
 // Buckets are padded to 16 B (4 uint32 or 8 uint16 entries) so the hot
 // kernel's 16-byte chunks never straddle two buckets; padding entries have C = 0.
 __global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, int64_t n,
@@ -838,8 +856,27 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   const bool p16 = shift <= kP16MaxShift;   // counts and offsets are in entries
   const uint32_t per16 = p16 ? 8u : 4u;
   const bool fused_parts = blk && n_targets > 0 && nblk <= kPartLds;
+  if (blk) {   // every counter, the status word and the tile minima in one launch
+    FillSet fs{};
+    int64_t longest = 1;
+    auto add = [&](void* ptr, int64_t n_words, uint32_t v) {
+      fs.p[fs.k] = static_cast<uint32_t*>(ptr);
+      fs.n[fs.k] = n_words;
+      fs.v[fs.k] = v;
+      ++fs.k;
+      longest = n_words > longest ? n_words : longest;
+    };
+    add(part_n, nblk + 1, 0u);
+    add(cntp, np + 1, 0u);
+    add(mxp, np + 1, 0u);
+    add(curp, np + 1, 0u);
+    if (status_dev) add(status_dev, 1, 0u);
+    if (tile_gmin && T > 0) add(tile_gmin, 2 * T, 0x7F7F7F7Fu);
+    if (tile_maxc) add(tile_maxc + nb, 1, 0u);
+    k_fill_set<<<grid_for(longest, kBlock), kBlock, 0, st>>>(fs);
+    DPS_LAUNCHED();
+  }
   if (fused_parts) {
-    DPS_HIP_RET(hipMemsetAsync(part_n, 0, (nblk + 1) * sizeof(uint32_t), st));
     k_invert_and_parts<<<grid_for(n_targets, kBlock, 1024), kBlock, 0, st>>>(
         t_rank, c_ptr, n_targets, lpb, static_cast<int>(nblk), perm, part_n);
     DPS_LAUNCHED();
@@ -848,21 +885,18 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     DPS_LAUNCHED();
   }
   const int32_t* perm_or_null = t_rank ? perm : nullptr;
-  if (status_dev) DPS_HIP_RET(hipMemsetAsync(status_dev, 0, sizeof(int32_t), st));
-  if (tile_gmin && T > 0) DPS_HIP_RET(hipMemsetAsync(tile_gmin, 0x7F, T * sizeof(int64_t), st));
+  if (!blk) {
+    if (status_dev) DPS_HIP_RET(hipMemsetAsync(status_dev, 0, sizeof(int32_t), st));
+    if (tile_gmin && T > 0) DPS_HIP_RET(hipMemsetAsync(tile_gmin, 0x7F, T * sizeof(int64_t), st));
+  }
   if (blk) {
-    DPS_HIP_RET(hipMemsetAsync(cntp, 0, (np + 1) * sizeof(uint32_t), st));
-    DPS_HIP_RET(hipMemsetAsync(mxp, 0, (np + 1) * sizeof(uint32_t), st));
-    DPS_HIP_RET(hipMemsetAsync(curp, 0, (np + 1) * sizeof(uint32_t), st));
     if (!fused_parts) {
-      DPS_HIP_RET(hipMemsetAsync(part_n, 0, (nblk + 1) * sizeof(uint32_t), st));
       if (n_targets > 0) {
         k_part_entries<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(c_ptr, perm_or_null,
                                                                        n_targets, lpb, part_n);
         DPS_LAUNCHED();
       }
     }
-    if (tile_maxc) DPS_HIP_RET(hipMemsetAsync(tile_maxc + nb, 0, sizeof(uint32_t), st));
     if (n_targets > 0 && nb > 0) {
       k_tile_count_blk<<<static_cast<unsigned>(nblk * S * n_ranges), kBlkThreads, 0, st>>>(
           c_ptr, c_col, c_val, perm_or_null, tile_gmin ? g : nullptr, n_targets, n_mids, shift, T,
