@@ -139,6 +139,22 @@ __device__ __forceinline__ int wave_bitonic_sort(int v) {
   return v;
 }
 
+// ---- several dword ranges set in one launch (dps_scan.hip) ---------------------
+// Replaces a hipMemsetAsync per small array (each one a fill kernel of its own).
+struct FillSet {
+  uint32_t* p[8];
+  int64_t n[8];    // dwords
+  uint32_t v[8];
+  int k = 0;
+  void add(void* ptr, int64_t n_words, uint32_t value) {
+    p[k] = static_cast<uint32_t*>(ptr);
+    n[k] = n_words;
+    v[k] = value;
+    ++k;
+  }
+};
+hipError_t fill_set(const FillSet& s, hipStream_t stream);
+
 // ---- device-wide scans (dps_scan.hip) ------------------------------------------
 // out[0..n] = exclusive prefix sums of in[0..n), out[n] = total.  ws from
 // scan_workspace_size(n).  T in {int32_t, uint32_t, int64_t}.

@@ -1057,8 +1057,12 @@ int dps_extract_incidence(const int32_t* edge_src, const int32_t* edge_dst,
   DPS_REQUIRE(n_edges >= 0 && n_nodes >= 0, DPS_ERR_INVALID, "negative size");
   DPS_REQUIRE(n_ap && n_px, DPS_ERR_INVALID, "null count output");
   auto st = static_cast<hipStream_t>(stream);
-  DPS_HIP_RET(hipMemsetAsync(n_ap, 0, sizeof(int64_t), st));
-  DPS_HIP_RET(hipMemsetAsync(n_px, 0, sizeof(int64_t), st));
+  {
+    FillSet fs;   // both counters in one launch
+    fs.add(n_ap, 2, 0u);
+    fs.add(n_px, 2, 0u);
+    DPS_HIP_RET(fill_set(fs, st));
+  }
   if (n_edges == 0) return DPS_OK;
   DPS_REQUIRE(edge_src && edge_dst && edge_rel && node_type && node_rowid && node_colid &&
                   ap_row && ap_col && px_row && px_col,
@@ -1287,10 +1291,16 @@ int dps_walks_fused(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c
               DPS_ERR_INVALID, "bad sizes");
   DPS_REQUIRE(c_ptr && g && (n_mids == 0 || (s && n_v)), DPS_ERR_INVALID, "null array");
   auto st = static_cast<hipStream_t>(stream);
-  if (stats) DPS_HIP_RET(hipMemsetAsync(stats, 0, DPS_STATS_LEN * sizeof(int64_t), st));
+  {
+    FillSet fs;   // stats, s and n_v zeroed in one launch
+    if (stats) fs.add(stats, 2 * DPS_STATS_LEN, 0u);
+    if (n_mids > 0) {
+      fs.add(s, 2 * n_mids, 0u);
+      fs.add(n_v, n_mids, 0u);
+    }
+    DPS_HIP_RET(fill_set(fs, st));
+  }
   if (n_mids > 0) {
-    DPS_HIP_RET(hipMemsetAsync(s, 0, n_mids * sizeof(int64_t), st));
-    DPS_HIP_RET(hipMemsetAsync(n_v, 0, n_mids * sizeof(uint32_t), st));
     if (n_rows > 0 && n_mids > kSumLds) {
       k_col_sums_hash<<<1024, kBlock, 0, st>>>(c_ptr, c_col, c_val, n_rows,
                                                reinterpret_cast<unsigned long long*>(s),

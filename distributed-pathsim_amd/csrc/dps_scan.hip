@@ -126,4 +126,25 @@ template hipError_t scan_exclusive<uint32_t>(const uint32_t*, int64_t*, int64_t,
 template hipError_t scan_exclusive<int64_t>(const int64_t*, int64_t*, int64_t, void*, size_t,
                                             hipStream_t);
 
+namespace {
+__global__ __launch_bounds__(256) void k_fill_set(FillSet s) {
+  for (int r = 0; r < s.k; ++r) {
+    uint32_t* __restrict__ p = s.p[r];
+    const uint32_t v = s.v[r];
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < s.n[r];
+         i += static_cast<int64_t>(gridDim.x) * 256)
+      p[i] = v;
+  }
+}
+}  // namespace
+
+hipError_t fill_set(const FillSet& s, hipStream_t stream) {
+  if (s.k == 0) return hipSuccess;
+  int64_t longest = 1;
+  for (int r = 0; r < s.k; ++r) longest = s.n[r] > longest ? s.n[r] : longest;
+  const int64_t blocks = (longest + 255) / 256;
+  k_fill_set<<<static_cast<unsigned>(blocks < 4096 ? blocks : 4096), 256, 0, stream>>>(s);
+  return hipGetLastError();
+}
+
 }  // namespace dps

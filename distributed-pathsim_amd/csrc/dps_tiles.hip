@@ -122,24 +122,6 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
       if (gmin_s[i] != ~0ull) atomicMin(&gmin[i], gmin_s[i]);
 }
 
-// Up to eight dword ranges set to a value in one launch (the block-local build's
-// counters, status and tile minima: one kernel instead of a fill per array).
-struct FillSet {
-  uint32_t* p[8];
-  int64_t n[8];
-  uint32_t v[8];
-  int k;
-};
-__global__ __launch_bounds__(kBlock) void k_fill_set(FillSet s) {
-  for (int r = 0; r < s.k; ++r) {
-    uint32_t* __restrict__ p = s.p[r];
-    const uint32_t v = s.v[r];
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < s.n[r];
-         i += static_cast<int64_t>(gridDim.x) * kBlock)
-      p[i] = v;
-  }
-}
-
 // Buckets are padded to 16 B (4 uint32 or 8 uint16 entries) so the hot
 // kernel's 16-byte chunks never straddle two buckets; padding entries have C = 0.
 __global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, int64_t n,
@@ -857,24 +839,15 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   const uint32_t per16 = p16 ? 8u : 4u;
   const bool fused_parts = blk && n_targets > 0 && nblk <= kPartLds;
   if (blk) {   // every counter, the status word and the tile minima in one launch
-    FillSet fs{};
-    int64_t longest = 1;
-    auto add = [&](void* ptr, int64_t n_words, uint32_t v) {
-      fs.p[fs.k] = static_cast<uint32_t*>(ptr);
-      fs.n[fs.k] = n_words;
-      fs.v[fs.k] = v;
-      ++fs.k;
-      longest = n_words > longest ? n_words : longest;
-    };
-    add(part_n, nblk + 1, 0u);
-    add(cntp, np + 1, 0u);
-    add(mxp, np + 1, 0u);
-    add(curp, np + 1, 0u);
-    if (status_dev) add(status_dev, 1, 0u);
-    if (tile_gmin && T > 0) add(tile_gmin, 2 * T, 0x7F7F7F7Fu);
-    if (tile_maxc) add(tile_maxc + nb, 1, 0u);
-    k_fill_set<<<grid_for(longest, kBlock), kBlock, 0, st>>>(fs);
-    DPS_LAUNCHED();
+    FillSet fs;
+    fs.add(part_n, nblk + 1, 0u);
+    fs.add(cntp, np + 1, 0u);
+    fs.add(mxp, np + 1, 0u);
+    fs.add(curp, np + 1, 0u);
+    if (status_dev) fs.add(status_dev, 1, 0u);
+    if (tile_gmin && T > 0) fs.add(tile_gmin, 2 * T, 0x7F7F7F7Fu);
+    if (tile_maxc) fs.add(tile_maxc + nb, 1, 0u);
+    DPS_HIP_RET(fill_set(fs, st));
   }
   if (fused_parts) {
     k_invert_and_parts<<<grid_for(n_targets, kBlock, 1024), kBlock, 0, st>>>(
