@@ -1,6 +1,7 @@
 #!/bin/bash
 # config5 (top-100, two top-k registers per lane): 4 waves per SIMD (current)
-# vs 5 waves per SIMD with the register budget forced to 96 (ab/libdpathsim_w5k2.so).
+# vs 5 waves per SIMD with the register budget forced to 96 (ab/libdpathsim_w5k2.so,
+# built first with: tools/build_lean_variant.sh w5k2 -DDPS_W5_KPL=2).
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
