@@ -29,7 +29,12 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "distributed-pathsim_amd"))
 
-LDS_PEAK_GBS = 256 * 256 * 2.4   # B/clk/CU x CUs x GHz (MI355X_MICROARCH.md LDS)
+CLK_GHZ, N_CU = 2.4, 256
+# LDS bytes per clock per CU by instruction class (MI355X_MICROARCH.md §LDS):
+LDS_READ_B128 = 256.0    # ds_read_b128 (the accumulator read)
+LDS_WRITE_B128 = 79.0    # ds_write_b128 (zeroing the accumulator)
+LDS_ADD_B32 = 64.0       # ds_add_u32 = a b32-class store (the scatter)
+LDS_PEAK_GBS = LDS_READ_B128 * N_CU * CLK_GHZ   # b128-read-equivalent peak, GB/s
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -43,6 +48,8 @@ def parse():
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--tile-w", type=int, default=8192)
     ap.add_argument("--denominator", default="rowsum", choices=["rowsum", "diag"])
+    ap.add_argument("--venue-skip", type=int, default=None,
+                    help="1/0: force venue skipping on/off (default: the engine's)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r02", "pmc_hot.json"),
@@ -57,8 +64,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dpathsim.dist import (balanced_bounds, balanced_edges, gather_topk_compact, max_shard,
-                               pack_counts)
+    from dpathsim.dist import (RcclComm, balanced_bounds, balanced_edges, gather_topk_compact,
+                               max_shard, pack_counts)
     from dpathsim.engine import PathSimEngine
     from dpathsim.synth import CONFIGS, synth_config
 
@@ -66,17 +73,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs for the multi-rank path on a one-GPU box (never set by the
-    # driver): all ranks on one device, gloo instead of RCCL
+    # driver): all ranks on one device, the gather over gloo instead of RCCL
     local = int(os.environ.get("DPATHSIM_BENCH_DEVICE", local))
-    backend = os.environ.get("DPATHSIM_BENCH_BACKEND", "nccl")
-    if world > 1:
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+    backend = os.environ.get("DPATHSIM_BENCH_BACKEND", "rccl")
+    comm = None
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        # gloo carries the control plane only (RCCL unique id, barriers, the
+        # max over ranks of the step time); the top-k gather is RCCL over xGMI
+        # through libdpathsim's C ABI (dps_comm_init / dps_gather)
+        dist.init_process_group("gloo")
+        if backend == "rccl":
+            comm = RcclComm(device=dev)
 
     na_cfg, np_cfg, nm_cfg, mp_name, k_cfg = CONFIGS[args.config]
     k = args.k or k_cfg
@@ -85,7 +94,10 @@ def main():
     NA = typed.n_authors
 
     eng = PathSimEngine(typed, device=dev, tile_w=args.tile_w,
-                        denominator=args.denominator).upload()
+                        denominator=args.denominator)
+    if args.venue_skip is not None:
+        eng.venue_skip = bool(args.venue_skip) and args.denominator == "rowsum"
+    eng.upload()
 
     def plan():
         # contiguous row shards of equal estimated work (every rank derives the
@@ -130,7 +142,7 @@ def main():
             # the fp64 scores from its own g (the same exact division)
             pack_counts(out[0], out[1], out=packed)
             gather_topk_compact(packed, eng.tensor("den")[:NA], NA, world, out=gathered,
-                                bounds=bounds)
+                                bounds=bounds, comm=comm)
 
     for _ in range(args.warmup):
         step(False)
@@ -150,7 +162,7 @@ def main():
     if int(plan_mismatch.item()) != 0:
         raise RuntimeError("row shards changed between steps")
     if world > 1:
-        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        te = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         elapsed = float(te.item())
     ms_per_step = elapsed * 1e3 / args.steps
@@ -160,14 +172,17 @@ def main():
     # ---- roofline of the dominant kernel (dps_cct_topk -> k_cct1), measured live --
     # The kernel is bound by latency at the occupancy LDS capacity allows (5 waves
     # per SIMD, 8 KB of accumulator each); of the resources it uses the LDS array
-    # is the busiest (PMC, profiles/r02/pmc_hot.json), so the roofline is LDS:
-    # algorithmic LDS bytes per launch = 32 B per 16-byte chunk scattered (8
-    # ds_add_u32 of 4 B per lane) + 16 KiB per accumulator pass (8 KiB read + 8 KiB
-    # zeroed), both counted by the kernel itself (workspace words 1, 2), over the
-    # launch time measured with events on the kernel's stream; peak = 256 B/clk/CU
-    # (ds_read_b128 rate, MI355X_MICROARCH.md LDS) x 256 CUs x 2.4 GHz.
-    # HBM (secondary): 2 B per C^T entry x sum_{x in shard} sum_{v in x} n_v + the
-    # top-k output (20 B per slot) + row offsets, vs 8 TB/s.
+    # is the busiest (PMC), so the roofline is LDS, priced per instruction class
+    # (DESIGN.md §9): per launch the kernel counts its accumulator passes and the
+    # 16-byte chunks it scatters (workspace words 1, 2);
+    #   scatter  32 B per chunk of ds_add_u32 (b32 store class, 64 B/clk/CU),
+    #   read     8 KiB per pass of ds_read_b128 (256 B/clk/CU),
+    #   zero     8 KiB per pass of ds_write_b128 (79 B/clk/CU),
+    # floor = sum of bytes / rate / (256 CUs x 2.4 GHz); frac = floor / launch time
+    # (events on the kernel's stream).  `achieved` / `peak` express the same in
+    # b128-read-equivalent bytes (each class scaled by 256 / its rate).
+    # HBM (secondary, logical): 16 B per chunk scattered + 64 B per candidate
+    # completed from the heavy-venue table + 20 B per output slot + row offsets.
     topk_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_topk]))
     r0, r1 = bounds0[rank]
     shard = r1 - r0
@@ -179,13 +194,22 @@ def main():
     w[1:] = torch.cumsum(n_v[c_col], 0)
     terms = int((w[c_ptr[r1]] - w[c_ptr[r0]]).item())      # sum_{x in shard} sum_{v in x} n_v
     ent_bytes = 2 if args.tile_w <= 8192 else 4
-    bytes_launch = ent_bytes * terms + 20 * shard * k + 8 * (shard + 1)
+    kc = eng.kernel_counts()                         # the last launch's counts
+    n_pass, n_chunk, n_ver = kc["passes"], kc["chunks"], kc["verified"]
+    if n_chunk:
+        bytes_launch = 16 * n_chunk + 64 * n_ver + 20 * shard * k + 8 * (shard + 1)
+    else:   # kernels other than k_cct1 count nothing: every entry of the row's venues
+        bytes_launch = ent_bytes * terms + 20 * shard * k + 8 * (shard + 1)
     hbm_achieved = bytes_launch / (topk_ms * 1e-3) / 1e9
-    wsc = eng.tensor("topk_ws")[:24].view(torch.int64).cpu().tolist()   # last launch's counts
-    n_pass, n_chunk = int(wsc[1]), int(wsc[2])
-    lds_bytes = 32 * n_chunk + 16384 * n_pass
+    lds_cls = {"scatter_add_b32": 32 * n_chunk, "acc_read_b128": 8192 * n_pass,
+               "acc_zero_b128": 8192 * n_pass}
+    lds_rate = {"scatter_add_b32": LDS_ADD_B32, "acc_read_b128": LDS_READ_B128,
+                "acc_zero_b128": LDS_WRITE_B128}
+    lds_floor_ms = {c: b / lds_rate[c] / (N_CU * CLK_GHZ * 1e9) * 1e3 for c, b in lds_cls.items()}
+    lds_bytes = sum(lds_cls.values())
+    lds_equiv = sum(b * LDS_READ_B128 / lds_rate[c] for c, b in lds_cls.items())
     # only the lean W = 8192 kernel (k_cct1) counts its passes and chunks
-    lds_achieved = lds_bytes / (topk_ms * 1e-3) / 1e9 if n_pass > 0 else None
+    lds_achieved = lds_equiv / (topk_ms * 1e-3) / 1e9 if n_pass > 0 else None
     traffic, pmc = None, {}
     if args.pmc_json and os.path.exists(args.pmc_json):
         try:
@@ -290,13 +314,19 @@ def main():
             # bound: the busiest resource per the HEAD counters (LDS array; the
             # kernel is latency-bound at the occupancy its LDS allows)
             "roofline": {"bound": "lds", "kernel": "dps_cct_topk (k_cct1, W 8192)",
-                         "achieved": lds_achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
+                         "achieved": lds_achieved, "peak": LDS_PEAK_GBS,
+                         "unit": "GB/s (ds_read_b128-equivalent)",
                          "frac": lds_achieved / LDS_PEAK_GBS if lds_achieved else None,
                          "traffic": traffic,
-                         "lds_bytes": lds_bytes, "passes": n_pass, "chunks": n_chunk,
+                         "lds_bytes": lds_bytes, "lds_bytes_by_class": lds_cls,
+                         "lds_rate_B_per_clk_cu": lds_rate,
+                         "lds_floor_ms_by_class": lds_floor_ms,
+                         "lds_floor_ms": sum(lds_floor_ms.values()),
+                         "passes": n_pass, "chunks": n_chunk, "verified": n_ver,
+                         "venue_skip": eng._vskip is not None,
                          "avg_launch_ms": topk_ms,
                          "pmc": pmc,
-                         "hbm": {"algorithmic_bytes": bytes_launch, "bytes_per_entry": ent_bytes,
+                         "hbm": {"algorithmic_bytes": bytes_launch,
                                  "achieved": hbm_achieved, "peak": HBM_PEAK_GBS,
                                  "frac": hbm_achieved / HBM_PEAK_GBS,
                                  "traffic_frac": (traffic / (topk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
@@ -310,6 +340,8 @@ def main():
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
 
 

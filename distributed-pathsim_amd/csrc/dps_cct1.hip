@@ -23,6 +23,21 @@
 // Skipping a tile is sound for the same reason as in k_cct_topk: UB bounds
 // every M of the tile and mneed_lo32(tau, gx + gmin_t) is at most the
 // smallest M whose score can reach tau (ties included).
+//
+// Venue skipping (HV, the row-sum denominator only): every target y has
+// g[y] = sum_u C[y,u] s_u, so for a venue set H of row x,
+// M_H(y) = sum_{h in H} a_h b_h <= rho_H * g[y] with a = C[x,.], b = C[y,.] and
+// rho_H = max_{h in H} a_h / s_h.  Once the row's top-k is full (k-th score
+// tau), the heavy venues with 2 a_h <= tau s_h form H: their buckets are no
+// longer scattered, and score(y) >= tau needs
+//   M_Q(y) >= tau (gx + g[y]) / 2 - rho_H g[y]     (Q = the other venues),
+// whose right side does not decrease in g[y] (rho_H <= tau / 2), so the
+// segment's smallest g gives a sound per-segment threshold.  A target that
+// passes gets its exact M = M_Q + sum_{h in H} a_h C[y,h] from the dense
+// heavy-venue table hv_c (one cache line per target) before it is scored.
+// The heavy venues hold most of C^T's entries (config3: half of the chunks a
+// row scatters), and once every venue of a row is in H no target can reach
+// tau at all (score < 2 rho_H <= tau), so the row ends.
 // Three 64-chunk loads per batch (not the general kernel's four): with the
 // candidate queue in VGPRs it keeps the kernel within 96 VGPRs, 5 waves per SIMD.
 #ifndef DPS_KU
@@ -147,11 +162,14 @@ struct Stage1 {
   float gsf;     // lane s < 8: smallest g of segment s, as float
 };
 
-__device__ __forceinline__ void stage_make(Stage1& X, const Pend1& P, int c, int d0) {
+// hm: the venue lanes (H) whose buckets this stage skips (venue skipping).
+__device__ __forceinline__ void stage_make(Stage1& X, const Pend1& P, int c, int d0, uint64_t hm,
+                                           int lane) {
   X.S.t = P.t;
   X.S.lnp = P.ub <= 0xFFu ? 0 : P.ub <= 0xFFFFu ? 1 : 2;
   X.S.pass = 0;
-  grp_set(X.S.G, P.lo, P.hi, c, d0);
+  const bool skip = (hm >> lane) & 1ull;          // an H venue's bucket is not scattered
+  grp_set(X.S.G, P.lo, skip ? P.lo : P.hi, c, d0);
   X.S.nb = (X.S.G.nq + kWave * kU - 1) / (kWave * kU);
   X.S.gq = 0;
   X.gsf = i64_f32(P.gs);
@@ -165,7 +183,9 @@ __device__ __forceinline__ uint32_t ge_u8_lo(uint32_t a, uint32_t kA) {
 // Order the row's first 64 venues by their total bucket size, smallest first,
 // so a stage's small buckets sit together at the front of the flattened chunk
 // range (one vector load) and the large ones fill whole fast loads.
-__device__ __forceinline__ void sort_venues(const CctParams& p, int d0, int lane, int& c, uint32_t& vT) {
+template <bool HV>
+__device__ __forceinline__ void sort_venues(const CctParams& p, int d0, int lane, int& c, uint32_t& vT,
+                                            int& v) {
   int key = INT_MAX;
   if (lane < d0) {
     const uint32_t n = p.tile_off[vT + static_cast<uint32_t>(p.T)] - p.tile_off[vT];
@@ -174,7 +194,20 @@ __device__ __forceinline__ void sort_venues(const CctParams& p, int d0, int lane
   const int src = wave_bitonic_sort(key) & (kWave - 1);
   c = __shfl(c, src, kWave);
   vT = static_cast<uint32_t>(__shfl(static_cast<int>(vT), src, kWave));
+  if (HV) v = __shfl(v, src, kWave);
 }
+
+// Venue skipping state of venue lane j in one VGPR: the bits of an fp32 upper
+// bound of C[x,v] / s_v with the low 7 mantissa bits replaced by slot + 1 (0 =
+// not a heavy venue).  Rounding the ratio up to a multiple of 2^-16 relative
+// first keeps the packed value an upper bound.
+constexpr uint32_t kHvSlot = 0x7Fu;
+__device__ __forceinline__ uint32_t hv_pack(float ratio_up, int slot) {
+  if (slot < 0) return 0u;
+  const uint32_t b = (__float_as_uint(ratio_up) & ~kHvSlot) + (kHvSlot + 1u);
+  return b | static_cast<uint32_t>(slot + 1);
+}
+__device__ __forceinline__ float hv_ratio(uint32_t hv) { return __uint_as_float(hv); }
 
 // Candidate queue in VGPRs (no LDS: the wave's 8 KB of LDS is all
 // accumulator, so 20 waves fit a CU): slot s lives in lane s % 64, register
@@ -203,15 +236,30 @@ __device__ __forceinline__ void vq_push(VQ& Q, bool has, int lab, int m, uint64_
 
 // Exact score of the first n (<= 64) queued candidates; insert those that beat
 // the k-th entry; drop them from the queue (n == 64 moves slots 64.. down).
-template <int KPL>
+// Venue skipping: the queued counts miss the venues of hm (the H of the
+// stages that queued them); their exact share sum_{h in H} C[x,h] * C[y,h]
+// comes from the heavy-venue table (lane h holds C[x,h] in c and the venue's
+// table slot in the low bits of hv, see hv_pack).
+template <int KPL, bool HV>
 __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& top, int n,
-                                         int64_t gx, int lane) {
+                                         int64_t gx, int lane, int c, uint32_t hv, uint64_t hm,
+                                         uint32_t& nver) {
   bool cand = lane < n;
   int M = 0, yo = 0;
   double sc = 0.0;
+  if (HV && hm) {
+    nver += static_cast<uint32_t>(n);
+    const uint16_t* row = p.hv_c + static_cast<int64_t>(cand ? Q.lab0 : 0) * p.n_hv;
+    for (uint64_t m = hm; m; m &= m - 1) {          // wave-uniform, |H| is small
+      const int j = __builtin_ctzll(m);
+      const int a = readlane(c, j);
+      const int sl = static_cast<int>(readlane(hv, j) & kHvSlot) - 1;
+      if (cand) M += a * static_cast<int>(row[sl]);
+    }
+  }
   if (cand) {
     const int64_t label = Q.lab0;
-    M = Q.m0;
+    M += Q.m0;
     yo = p.t_perm ? p.t_perm[label] : static_cast<int>(label);
     const int64_t den = gx + p.g_t[label];
     sc = static_cast<double>(2 * static_cast<int64_t>(M)) / static_cast<double>(den);
@@ -233,10 +281,10 @@ __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& t
 // u16 / u32 pass epilogue (UB > 255, rare): scan + zero the accumulator of
 // pass `pass` (2 or 1 targets per dword), queue targets reaching their
 // segment's threshold.
-template <int KPL>
+template <int KPL, bool HV>
 __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                           const Stage& S, int lane, int64_t x_lab, int64_t gx,
-                                          int mseg) {
+                                          int mseg, int c, uint32_t hv, uint64_t hm, uint32_t& nver) {
   const int lnp = S.lnp;
   const int tpd_shift = 2 - lnp;                     // log2(targets per dword)
   const int bits = 8 << lnp;
@@ -261,7 +309,7 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
       const uint64_t mk = ballot(cand);
       if (!mk) continue;
       vq_push(Q, cand, static_cast<int>(label), static_cast<int>(M), mk, lane);
-      if (Q.n >= kWave) vq_flush<KPL>(p, Q, top, kWave, gx, lane);
+      if (Q.n >= kWave) vq_flush<KPL, HV>(p, Q, top, kWave, gx, lane, c, hv, hm, nver);
     }
   }
 }
@@ -269,9 +317,10 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
 // u8 epilogue over the whole tile: 8 blocks of 1024 targets (one threshold
 // segment each, lane l reads dwords 4l..4l+3 of the block), read and zeroed 4
 // at a time; candidates are queued and scored 64 at a time by flush().
-template <int KPL>
+template <int KPL, bool HV>
 __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
-                                        int t, int lane, int64_t x_lab, int64_t gx, int mseg) {
+                                        int t, int lane, int64_t x_lab, int64_t gx, int mseg,
+                                        int c, uint32_t hv, uint64_t hm, uint32_t& nver) {
   const int64_t tile_base = static_cast<int64_t>(t) << kS1;
   const int64_t xr = x_lab - tile_base;
   const bool xin = xr >= 0 && xr < kW1;          // the source is a target of this tile
@@ -314,7 +363,7 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
         mv = static_cast<int>((wv >> (byte * 8)) & 0xFFu);
       }
       vq_push(Q, has, lab, mv, mk, lane);
-      if (Q.n >= kWave) vq_flush<KPL>(p, Q, top, kWave, gx, lane);
+      if (Q.n >= kWave) vq_flush<KPL, HV>(p, Q, top, kWave, gx, lane, c, hv, hm, nver);
     }
   };
 #pragma unroll 1
@@ -417,7 +466,7 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
 #ifndef DPS_W5_KPL
 #define DPS_W5_KPL 1
 #endif
-template <int KPL>
+template <int KPL, bool HV>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DPS_W5_KPL ? 5 : 4))) void k_cct1(CctParams p) {
   // LDS: the accumulator at address 0 (scatter ORs the in-tile offset into 0)
   // then the candidate queue.
@@ -438,6 +487,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
   // accumulator passes (each reads and zeroes the 8 KiB accumulator) and 16-byte
   // chunks scattered -- the bench's algorithmic LDS bytes
   uint64_t n_pass = 0, n_chunk = 0;
+  uint32_t n_ver = 0;   // candidates completed from the heavy-venue table (counter[3])
 
   for (;;) {
     unsigned long long rr = 0;
@@ -460,13 +510,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
 
     if (d > 0 && t_beg < t_end) {
       const int d0 = d < kWave ? d : kWave;
-      int c = 0;
+      int c = 0, v = 0;
       uint32_t vT = 0;
       if (lane < d0) {
         c = p.c_val[pb + lane];
-        vT = static_cast<uint32_t>(p.c_col[pb + lane]) * static_cast<uint32_t>(p.T);
+        v = p.c_col[pb + lane];
+        vT = static_cast<uint32_t>(v) * static_cast<uint32_t>(p.T);
       }
-      if (d0 > 1) sort_venues(p, d0, lane, c, vT);
+      if (d0 > 1) sort_venues<HV>(p, d0, lane, c, vT, v);
+      // venue skipping: lane j < d0 holds venue j's heavy-table slot (-1: none)
+      // and an upper bound of C[x,v] / s_v (s_v >= C[x,v] > 0)
+      uint32_t hv = 0;          // hv_pack(C[x,v] / s_v rounded up, slot)
+      uint64_t hm = 0;          // H: venue lanes no longer scattered
+      if (HV && lane < d0) {
+        const int sl = p.hv_slot[v];
+        if (sl >= 0)
+          hv = hv_pack(static_cast<float>(static_cast<double>(c) / static_cast<double>(p.s[v])) *
+                           (1.0f + 0x1p-20f), sl);
+      }
       Win1 w;
       win_load(p, w, t_beg, t_beg, t_end, pb, d, c, vT, lane, -1.0, gxf);
       uint32_t ub_t = 0;
@@ -475,7 +536,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
         Pend1 P;
         pend_load(p, P, t0, ub_t, d0, vT, lane);
         Stage1 X;
-        stage_make(X, P, c, d0);
+        stage_make(X, P, c, d0, 0ull, lane);
+        bool hchg = false;        // H grew at the last stage boundary
         Batch B;
         issue1(X.S, 0, p.tile_ent, lane, B);
         const int t1 = next_tile(p, w, t_end, pb, d, c, vT, lane, -1.0, gxf, ub_t);
@@ -499,25 +561,50 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
             // score what is queued while the list is filling or the queue is
             // half full (one memory round trip per 64 candidates)
             if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
-              vq_flush<KPL>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane);
+              vq_flush<KPL, HV>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane, c, hv, hm, n_ver);
             const double tau = top.full() ? top.kth_s : -1.0;
             int mseg = 1;
             if (tau > 0.0) {
-              const int mn = mneed_lo32(static_cast<float>(tau), gxf + X.gsf);
-              mseg = mn > 1 ? mn : 1;
+              if (HV && hm) {
+                // M_Q >= tau (gx + gs) / 2 - rho gs, rounded down (fp32, every
+                // rounding to nearest; the factors keep it below the exact value)
+                float rho = 0.0f;   // >= max_{h in H} C[x,h] / s_h
+                for (uint64_t m = hm; m; m &= m - 1)
+                  rho = fmaxf(rho, hv_ratio(readlane(hv, __builtin_ctzll(m))));
+                const float gs = X.gsf;
+                const float r = static_cast<float>(tau) * (gxf + gs) * (0.5f * (1.0f - 0x1p-19f)) -
+                                rho * gs * (1.0f + 0x1p-17f);
+                mseg = r >= 2147483000.0f ? INT32_MAX : r > 1.0f ? static_cast<int>(ceilf(r)) : 1;
+              } else {
+                const int mn = mneed_lo32(static_cast<float>(tau), gxf + X.gsf);
+                mseg = mn > 1 ? mn : 1;
+              }
             }
             const bool last = X.S.pass + 1 == npass;
             Stage S = X.S;
+            const uint64_t hmS = hm;   // this stage's H (the update below is for the next)
             if (prof) ts[2] = __builtin_amdgcn_s_memtime();
             if (last) {
               // next stage: its bounds were loaded one stage ago; put its first
               // chunks in flight, then load the bounds of the one after
+              bool row_done = false;
+              hchg = false;
               if (tau > w.tau) {
                 w.live &= win_pass(w, tau, gxf);
                 w.tau = tau;
+                if (HV) {
+                  // H = the heavy venues with C[x,h] / s_h <= tau / 2 (hr is an
+                  // upper bound of the ratio, th a lower bound of tau / 2); with
+                  // every venue in H no target can reach tau
+                  const float th = static_cast<float>(tau) * (0.5f * (1.0f - 0x1p-20f));
+                  const uint64_t h2 = ballot(hv != 0u && hv_ratio(hv) <= th);
+                  hchg = h2 != hm;
+                  hm = h2;
+                  row_done = d <= kWave && hm == ballot(lane < d0);
+                }
               }
-              more = P.t >= 0;
-              if (more) stage_make(X, P, c, d0);
+              more = P.t >= 0 && !row_done;
+              if (more) stage_make(X, P, c, d0, hm, lane);
               else X.S.G.nq = 0;
               if (prof) ts[5] = __builtin_amdgcn_s_memtime();
               issue1(X.S, 0, p.tile_ent, lane, B);
@@ -527,10 +614,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
             }
             if (prof) ts[3] = __builtin_amdgcn_s_memtime();
             if (S.lnp == 0) {
-              epi1_u8<KPL>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg);
+              epi1_u8<KPL, HV>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
+                               hmS, n_ver);
             } else {
-              epi1_wide<KPL>(p, acc, top, Q, S, lane, x_lab, gx, mseg);
+              epi1_wide<KPL, HV>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, n_ver);
             }
+            // the queue holds counts that miss hmS: complete them before the
+            // next stage's (larger) H applies
+            if (HV && hchg)
+              while (Q.n > 0)
+                vq_flush<KPL, HV>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane, c, hv, hmS, n_ver);
             if (prof) {
               ts[4] = __builtin_amdgcn_s_memtime();
 #pragma unroll
@@ -543,8 +636,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
           if (!more) break;
         }
       }
+      while (Q.n > 0) vq_flush<KPL, HV>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane, c, hv, hm, n_ver);
     }
-    while (Q.n > 0) vq_flush<KPL>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane);
 
     // ranked entries, then zero-score targets in reference order, then -1
     int32_t* oi = (is_piece ? p.piece_idx : p.out_idx) + ro * p.k;
@@ -585,6 +678,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
   if (lane == 0 && (n_pass | n_chunk)) {
     atomicAdd(p.counter + 1, static_cast<unsigned long long>(n_pass));
     atomicAdd(p.counter + 2, static_cast<unsigned long long>(n_chunk));
+    if (HV && n_ver) atomicAdd(p.counter + 3, static_cast<unsigned long long>(n_ver));
   }
   if (prof && lane == 0) {
 #pragma unroll
@@ -598,11 +692,14 @@ int launch1(const CctParams& p, hipStream_t st) {
   DPS_HIP_RET(hipGetDevice(&dev));
   DPS_HIP_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
   int wpc = KPL <= DPS_W5_KPL ? 20 : 16;   // 5 or 4 waves per SIMD, 8 KB of LDS each
+#ifdef DPS_PROFILE
   if (const char* e = std::getenv("DPATHSIM_LEAN_WPC")) wpc = std::atoi(e);   // experiments
   if (wpc < 1 || wpc > 20) wpc = 20;
+#endif
   int64_t grid = static_cast<int64_t>(n_cu) * wpc;
   if (grid > p.n_rows) grid = p.n_rows;
-  k_cct1<KPL><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  if (p.hv_c) k_cct1<KPL, true><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  else k_cct1<KPL, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
   DPS_LAUNCHED();
   return DPS_OK;
 }

@@ -46,6 +46,13 @@ struct CctParams {
   bool dbuf;                 // two alternating stage buffers (W <= 16384) or one
   int ablate;                // profiling aid (DPATHSIM_ABLATE, -DDPS_PROFILE builds only):
                              // 1 no LDS adds, 2 no candidate scoring, 4 no scatter
+  // venue skipping (lean kernel, dps_venue_skip in dpathsim.h; all null = off):
+  // s[v] the global-walk weights, hv_slot[v] the heavy-venue slot or -1,
+  // hv_c[label * n_hv + slot] = C[y, venue of slot] for target label(y)
+  const int64_t* s;
+  const int32_t* hv_slot;
+  const uint16_t* hv_c;
+  int n_hv;
 };
 
 // Lean one-wave kernel for W = 8192 (dps_cct1.hip).

@@ -1124,8 +1124,11 @@ int dps_csr_build(const int32_t* rows, const int32_t* cols, int64_t n_pairs,
   DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "csr_build workspace carve failed");
 
   const BucketPlan B = bucket_plan(n_pairs, n_rows);
-  const char* env = std::getenv("DPATHSIM_CSR_ATOMIC");   // A/B: the per-pair atomic path
-  if (B.ok && !(env && std::atoi(env) != 0)) {
+  bool atomic_path = false;   // A/B (profiling build only): the per-pair atomic path
+#ifdef DPS_PROFILE
+  if (const char* env = std::getenv("DPATHSIM_CSR_ATOMIC")) atomic_path = std::atoi(env) != 0;
+#endif
+  if (B.ok && !atomic_path) {
     DPS_REQUIRE(rows && cols, DPS_ERR_INVALID, "null input pairs");
     const int64_t nh = static_cast<int64_t>(B.n_buckets) * B.n_blocks;
     uint32_t* H = c.take<uint32_t>(nh + 1);

@@ -141,16 +141,42 @@ const Attr* find(const std::vector<Attr>& a, std::string_view n) {
   return nullptr;
 }
 
+// True unless [b, e) is an XML declaration naming an encoding other than
+// UTF-8 / ASCII (those files go to the caller's parser, which decodes them).
+bool utf8_declaration(const char* b, const char* e) {
+  const std::string_view d(b, static_cast<size_t>(e - b));
+  if (d.substr(0, 5) != "<?xml") return true;
+  const size_t k = d.find("encoding");
+  if (k == std::string_view::npos) return true;
+  size_t i = k + 8;
+  while (i < d.size() && (d[i] == ' ' || d[i] == '=' || d[i] == '\t')) ++i;
+  if (i >= d.size() || (d[i] != '"' && d[i] != '\'')) return false;
+  const char q = d[i++];
+  const size_t j = d.find(q, i);
+  if (j == std::string_view::npos) return false;
+  std::string enc(d.substr(i, j - i));
+  for (char& c : enc) c = static_cast<char>(c >= 'A' && c <= 'Z' ? c - 'A' + 'a' : c);
+  return enc == "utf-8" || enc == "utf8" || enc == "ascii" || enc == "us-ascii";
+}
+
 class Scanner {
  public:
   Scanner(const char* b, const char* e, Gexf& g) : p_(b), e_(e), g_(g) {}
 
   int run() {
+    // byte-order marks of UTF-16/32: not this scanner's encoding
+    if (e_ - p_ >= 2 && ((p_[0] == '\xFF' && p_[1] == '\xFE') || (p_[0] == '\xFE' && p_[1] == '\xFF')))
+      return kFallback;
     while (p_ < e_) {
       const char* lt = static_cast<const char*>(std::memchr(p_, '<', static_cast<size_t>(e_ - p_)));
       if (!lt) break;
       p_ = lt;
-      if (e_ - p_ >= 2 && p_[1] == '?') { if (!skip_to("?>")) return kFallback; continue; }
+      if (e_ - p_ >= 2 && p_[1] == '?') {
+        const char* q0 = p_;
+        if (!skip_to("?>")) return kFallback;
+        if (!utf8_declaration(q0, p_)) return kFallback;
+        continue;
+      }
       if (starts("<!--")) { if (!skip_to("-->")) return kFallback; continue; }
       if (starts("<![CDATA[")) { if (!skip_to("]]>")) return kFallback; continue; }
       if (e_ - p_ >= 2 && p_[1] == '!') return kFallback;   // DOCTYPE / declarations

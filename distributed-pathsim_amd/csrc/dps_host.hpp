@@ -6,6 +6,8 @@
 
 namespace dps {
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+// current dps_set_tuning value of `key` (0 = automatic)
+int tuning(int key);
 }  // namespace dps
 
 #define DPS_REQUIRE(cond, code, ...)                                                   \

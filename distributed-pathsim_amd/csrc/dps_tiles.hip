@@ -699,12 +699,14 @@ int log2_exact(int32_t w) {
 }
 
 // Labels per block of the block-local build: a power of two in [1024, tile_w]
-// (DPATHSIM_TILE_LPB overrides the default, for A/B runs).  Every block writes
+// (DPATHSIM_TILE_LPB overrides the default in the -DDPS_PROFILE build, for A/B runs).  Every block writes
 // one count slot per (mid, part), so fewer, wider parts shrink the slot arrays
 // and their scan; more parts give more blocks.
 int tile_lpb(int32_t tile_w) {
   int lpb = kBlkLabels;
+#ifdef DPS_PROFILE
   if (const char* e = std::getenv("DPATHSIM_TILE_LPB")) lpb = std::atoi(e);
+#endif
   if (lpb < 1024 || lpb > kBlkLabels || (lpb & (lpb - 1))) lpb = kBlkLabels;
   return tile_w < lpb ? tile_w : lpb;
 }
@@ -712,7 +714,9 @@ int tile_lpb(int32_t tile_w) {
 // Sub-blocks per part of the block-local build (entries split evenly).
 int tile_sub() {
   int sub = kBlkSub;
+#ifdef DPS_PROFILE
   if (const char* e = std::getenv("DPATHSIM_TILE_SUB")) sub = std::atoi(e);
+#endif
   return sub < 1 || sub > 64 ? kBlkSub : sub;
 }
 
@@ -720,11 +724,14 @@ int tile_sub() {
 // per mid range reads C once per range, so it is taken up to kMaxMidRanges
 // ranges (config5, 20k venues, 3 ranges: 7.1 -> 2.8 ms) and the global-atomic
 // counting sort above (config4, 200k topics, 25 ranges: 7.5 vs 13.7 ms);
-// DPATHSIM_TILE_GLOBAL=1 / 0 forces one or the other.
+// DPATHSIM_TILE_GLOBAL=1 / 0 forces one or the other (-DDPS_PROFILE build).
 constexpr int64_t kMaxMidRanges = 8;
 bool tile_global(int64_t n_mids) {
   if (n_mids <= kBlkMids) return false;
+  if (const int t = tuning(DPS_TUNE_TILE_BUILD)) return t == 2;
+#ifdef DPS_PROFILE
   if (const char* e = std::getenv("DPATHSIM_TILE_GLOBAL")) return std::atoi(e) != 0;
+#endif
   return (n_mids + kBlkMids - 1) / kBlkMids > kMaxMidRanges;
 }
 

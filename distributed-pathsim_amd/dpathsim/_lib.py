@@ -25,6 +25,14 @@ R_OTHER, R_AP, R_PX = 0, 1, 2
 STAT_MAX_C, STAT_MAX_DIAG, STAT_MAX_G, STAT_NNZ_C = 0, 1, 2, 3
 STATS_LEN = 8
 
+TUNE_WAVES_PER_ROW, TUNE_TILE_BUILD = 1, 2
+
+
+class VenueSkip(C.Structure):
+    """struct dps_venue_skip (include/dpathsim.h): device pointers + n_hv."""
+    _fields_ = [("s", C.c_void_p), ("hv_slot", C.c_void_p), ("hv_c", C.c_void_p),
+                ("n_hv", C.c_int32)]
+
 _i32 = C.c_int32
 _i64 = C.c_int64
 _sz = C.c_size_t
@@ -68,13 +76,23 @@ SIGNATURES = {
     "dps_ct_tiles_build": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p,
                                      _p, _sz, _p]),
     "dps_cct_topk_workspace_size": (_sz, []),
-    "dps_cct_topk": (C.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p,
+    "dps_cct_topk": (C.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p,
                                _i64, _i64, _p, _i32, _p, _p, _p, _p, _sz, _p]),
     "dps_cct_topk_rows": (C.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p,
-                                    _p, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
+                                    _p, _p, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "dps_cct_topk_split": (C.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p,
-                                     _p, _i64, _i64, _p, _i64, _p, _p, _i64, _p, _p, _p, _i32, _p,
-                                     _p, _p, _p, _sz, _p]),
+                                     _p, _p, _i64, _i64, _p, _i64, _p, _p, _i64, _p, _p, _p, _i32,
+                                     _p, _p, _p, _p, _sz, _p]),
+    "dps_heavy_venues": (C.c_int, [_p, _i64, _i32, _p, _p]),
+    "dps_heavy_table": (C.c_int, [_p, _p, _p, _p, _i64, _p, _i32, _p, _p]),
+    "dps_set_tuning": (C.c_int, [_i32, _i32]),
+    "dps_comm_id_bytes": (C.c_int, []),
+    "dps_comm_get_id": (C.c_int, [_p]),
+    "dps_comm_init": (C.c_int, [_p, _i32, _i32, _p]),
+    "dps_comm_destroy": (C.c_int, [_p]),
+    "dps_bcast": (C.c_int, [_p, _p, _sz, _i32, _p]),
+    "dps_gather": (C.c_int, [_p, _p, _p, _sz, _i32, _p]),
+    "dps_get_tuning": (C.c_int, [_i32]),
     "dps_topk_merge": (C.c_int, [_p, _p, _p, _p, _i64, _i32, _i32, _i64, _i64, _p, _p, _p, _p]),
     "dps_heavy_first_workspace_size": (_sz, [_i64]),
     "dps_heavy_first": (C.c_int, [_p, _i64, _i64, _i64, _i32, _p, _p, _sz, _p]),

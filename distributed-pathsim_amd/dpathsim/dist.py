@@ -2,8 +2,11 @@
 
 Every source row's top-k depends only on that row of C plus all of C and g,
 so ranks split the author rows into contiguous, work-balanced shards and
-exchange nothing but the finished top-k blocks.  One process per GPU; the
-collective is RCCL (``nccl`` backend) on the GPU box and gloo in the CPU tests.
+exchange nothing but the finished top-k blocks.  One process per GPU; on the
+GPU box the collective is RCCL over xGMI called through libdpathsim's C ABI
+(:class:`RcclComm`, dps_comm_* / dps_gather -- torch.distributed only carries
+the 128-byte unique id at start-up and the barriers), and gloo in the CPU
+tests.
 
 Results travel as ONE packed int64 buffer per rank, ``[rows, 2k]``: word 0..k-1
 holds (count << 32) | target index, word k..2k-1 the score's fp64 bits (16 B
@@ -14,12 +17,76 @@ in row order when the result is too large for one host (config 5: 3M x top-100).
 """
 from __future__ import annotations
 
+import ctypes as C
 import json
 import os
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+
+class RcclComm:
+    """An RCCL communicator owned by libdpathsim (dps_comm_init: one rank per
+    process, on the current device).  Rank 0 creates the unique id
+    (dps_comm_get_id); ``group`` -- any torch.distributed group, e.g. gloo --
+    only broadcasts those bytes.  Collectives run on the caller's current HIP
+    stream (dps_gather / dps_bcast)."""
+
+    def __init__(self, group=None, device=None):
+        from . import _lib
+        self._lib = _lib
+        lib = _lib.load()
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = (torch.device("cuda", torch.cuda.current_device()) if device is None
+                       else torch.device(device))
+        nb = int(lib.dps_comm_id_bytes())
+        buf = (C.c_uint8 * nb)()
+        if self.rank == 0:
+            _lib.call("dps_comm_get_id", C.addressof(buf))
+        cpu = dist.get_backend(group) != "nccl"
+        t = torch.tensor(bytearray(buf), dtype=torch.uint8,
+                         device="cpu" if cpu else self.device)
+        dist.broadcast(t, src=0, group=group)
+        buf = (C.c_uint8 * nb)(*t.cpu().tolist())
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.call("dps_comm_init", C.addressof(h), self.world, self.rank, C.addressof(buf))
+        self._h = h
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def gather(self, send: torch.Tensor, recv: torch.Tensor | None, root: int = 0):
+        """Every rank's ``send`` bytes into ``recv`` on ``root`` (rank r at
+        byte offset r * send.nbytes); device tensors, current stream."""
+        send = send.contiguous()
+        nb = send.numel() * send.element_size()
+        if self.rank == root:
+            if recv is None or recv.numel() * recv.element_size() < self.world * nb:
+                raise ValueError("receive buffer smaller than world * send bytes")
+        with torch.cuda.device(self.device):
+            self._lib.call("dps_gather", self._h, send.data_ptr(),
+                           recv.data_ptr() if recv is not None else None, nb, root, self._stream())
+        return recv
+
+    def bcast(self, buf: torch.Tensor, root: int = 0):
+        with torch.cuda.device(self.device):
+            self._lib.call("dps_bcast", self._h, buf.data_ptr(), buf.numel() * buf.element_size(),
+                           root, self._stream())
+        return buf
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.call("dps_comm_destroy", self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def shard_bounds(n_rows: int, rank: int, world: int) -> tuple[int, int]:
@@ -150,13 +217,15 @@ def rescore(packed: torch.Tensor, den: torch.Tensor, row_begin: int = 0):
 
 
 def gather_topk_compact(parts, den: torch.Tensor, n_rows: int, world: int, group=None,
-                        out=None, bounds=None, dst: int = 0, force_collective: bool = False):
+                        out=None, bounds=None, dst: int = 0, force_collective: bool = False,
+                        comm: RcclComm | None = None):
     """As :func:`gather_topk`, with 8 B per slot on the wire: every rank sends
     (count << 32) | index words; rank ``dst`` rebuilds the scores from its own
     copy of the denominator term ``den`` (every rank holds all of g).  ``parts``:
     (idx, cnt[, score]) [max_shard, k] or packed int64 [max_shard, k].
-    ``force_collective`` runs the gather even for one rank (lets a one-GPU box
-    exercise the RCCL call)."""
+    ``comm``: gather with libdpathsim's RCCL communicator (dps_gather) instead
+    of torch.distributed.  ``force_collective`` runs the gather even for one
+    rank (lets a one-GPU box exercise the RCCL call)."""
     if bounds is None:
         bounds = [shard_bounds(n_rows, r, world) for r in range(world)]
     packed = parts if isinstance(parts, torch.Tensor) else pack_counts(parts[0], parts[1])
@@ -165,6 +234,14 @@ def gather_topk_compact(parts, den: torch.Tensor, n_rows: int, world: int, group
     m = max_shard(n_rows, world, bounds)
     if packed.shape[0] != m:
         raise ValueError(f"part has {packed.shape[0]} rows, expected max_shard {m}")
+    if comm is not None:
+        if comm.rank == dst and (out is None or out.numel() < world * m * packed.shape[1]):
+            out = torch.empty((world * m, packed.shape[1]), dtype=torch.int64, device=packed.device)
+        comm.gather(packed, out if comm.rank == dst else None, root=dst)
+        if comm.rank != dst:
+            return None
+        full = torch.cat([out[r * m: r * m + (b - a)] for r, (a, b) in enumerate(bounds)])
+        return rescore(full, den)
     rank = dist.get_rank(group)
     nccl = dist.get_backend(group) == "nccl"
     src = packed.contiguous() if nccl else packed.contiguous().cpu()

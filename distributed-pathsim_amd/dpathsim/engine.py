@@ -6,6 +6,7 @@ queries of DPathSim_APVPA.py:70-109 (see include/dpathsim.h per entry point).
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 import os
 import time
@@ -20,6 +21,10 @@ from .graph import TypedTables
 DEFAULT_TILE_W = 8192
 DEFAULT_SPLIT_ROWS = 256    # heaviest rows of a launch cut into pieces
 DEFAULT_PIECES = 16         # target-tile ranges per split row
+DEFAULT_HEAVY_VENUES = 32   # venue skipping: heavy venues in the dense table (64-byte rows)
+# venue skipping is exact but, on config3, 41 % fewer chunks scattered still
+# took 89.4 ms against 86.9 ms without it (profiles/r03/a): off by default
+DEFAULT_VENUE_SKIP = False
 
 
 def _ptr(t):
@@ -82,6 +87,12 @@ class PathSimEngine:
         self.tile_w = int(tile_w)
         self.denominator = denominator
         self.tile_skip = True
+        # multi-mid SpGEMM: "sort" (expand + segmented sort/unique) or "hash"
+        self.spgemm = "sort"
+        # venue skipping (dps_venue_skip): exact, row-sum denominator only
+        self.venue_skip = DEFAULT_VENUE_SKIP and denominator == "rowsum"
+        self.n_heavy = DEFAULT_HEAVY_VENUES
+        self._vskip = None
         # load balance of the hot kernel: the split_rows heaviest rows of a
         # launch are cut into `pieces` target-tile ranges (see topk())
         self.split_rows = DEFAULT_SPLIT_ROWS
@@ -191,7 +202,7 @@ class PathSimEngine:
             # raw-edge bounds (sum_c >= nnz C), no size read-back.  Papers with
             # at most one mid (APVPA): gather + segmented unique; otherwise
             # expand + segmented sort/unique (config4: 3.2 ms against 9.8 ms for
-            # the hash SpGEMM, kept behind DPATHSIM_SPGEMM=hash).
+            # the hash SpGEMM, kept as engine.spgemm = "hash").
             cap = bnd.sum_c
             c_ptr, c_nnz = self._empty(NR + 1, torch.int64), self._empty(2, torch.int64)
             sp_status = self._empty(1, torch.int32)
@@ -205,7 +216,7 @@ class PathSimEngine:
                               _ptr(c_val) if numeric else None, _ptr(c_nnz), _ptr(sws),
                               sws.numel(), st)
                 del vp
-            elif os.environ.get("DPATHSIM_SPGEMM", "sort") == "sort":
+            elif self.spgemm != "hash":
                 # expand + segmented sort/unique (sum_c bounds the expansion)
                 sws = self._ws(_lib.size("dps_spgemm_workspace_size", NR, bnd.sum_c))
                 sp_status.zero_()
@@ -262,13 +273,27 @@ class PathSimEngine:
                       _ptr(tile_maxc), _ptr(tile_gmin), _ptr(status), _ptr(tws), tws.numel(), st)
             mark("tiles")
             del tws
+            hv_slot = hv_c = None
+            if self.venue_skip and self.denominator == "rowsum" and NA and NV:
+                # venue skipping: the heavy venues (most author entries) and the
+                # dense table of C over them, by target label
+                nh = min(self.n_heavy, 64)
+                hv_slot = self._empty(NV, torch.int32)
+                hv_c = self._empty(NA * nh, torch.int16)
+                _lib.call("dps_heavy_venues", _ptr(n_v), NV, nh, _ptr(hv_slot), st)
+                _lib.call("dps_heavy_table", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(t_rank), NA,
+                          _ptr(hv_slot), nh, _ptr(hv_c), st)
+                mark("heavy")
         d.pop("row_work", None)
         d.update(row_terms=terms, ap_ptr=ap_ptr, ap_col=ap_col, px_ptr=px_ptr, px_col=px_col, c_ptr=c_ptr,
                  c_col=c_col, c_val=c_val, c_nnz=c_nnz, s=s, g=g, diag=diag, den=den, g_t=g_t,
                  t_perm=t_perm, t_rank=t_rank, tile_off=tile_off, tile_ent=tile_ent,
                  tile_maxc=tile_maxc, tile_gmin=tile_gmin, stats=stats, status=status,
-                 ap_nnz=ap_nnz, px_nnz=px_nnz, sp_status=sp_status,
+                 ap_nnz=ap_nnz, px_nnz=px_nnz, sp_status=sp_status, hv_slot=hv_slot, hv_c=hv_c,
                  topk_ws=self._ws(_lib.size("dps_cct_topk_workspace_size")))
+        self._vskip = None
+        if hv_c is not None:
+            self._vskip = _lib.VenueSkip(_ptr(s), _ptr(hv_slot), _ptr(hv_c), min(self.n_heavy, 64))
         self.built = True
         if timed:
             torch.cuda.synchronize(self.device)
@@ -315,6 +340,20 @@ class PathSimEngine:
     # ------------------------------------------------------------- accessors
     def tensor(self, name):
         return self._dev[name]
+
+    def kernel_counts(self):
+        """Work counts of the last W = 8192 hot-kernel launch (its workspace):
+        rows dequeued, accumulator passes, 16-byte chunks scattered, candidates
+        completed from the heavy-venue table (venue skipping)."""
+        w = self._dev["topk_ws"][:32].view(torch.int64).cpu().tolist()
+        return {"dequeued": int(w[0]), "passes": int(w[1]), "chunks": int(w[2]),
+                "verified": int(w[3])}
+
+    def _vskip_arg(self):
+        """Host pointer to the dps_venue_skip struct (None = off)."""
+        if self._vskip is None or not self.venue_skip:
+            return None
+        return C.addressof(self._vskip)
 
     @property
     def n_targets(self):
@@ -369,7 +408,8 @@ class PathSimEngine:
         common = (_ptr(d["c_ptr"]), _ptr(d["c_col"]), _ptr(d["c_val"]), _ptr(d["den"]),
                   _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA, self.typed.n_mids,
                   self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
-                  _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]))
+                  _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]),
+                  self._vskip_arg())
         with torch.cuda.device(self.device):
             dq = None
             if heavy_first and R > 1:
@@ -427,7 +467,7 @@ class PathSimEngine:
                       _ptr(d["den"]), _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA,
                       self.typed.n_mids, self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
                       _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]),
-                      _ptr(order), R, int(k), _ptr(tmp[0]), _ptr(tmp[1]), _ptr(tmp[2]),
+                      self._vskip_arg(), _ptr(order), R, int(k), _ptr(tmp[0]), _ptr(tmp[1]), _ptr(tmp[2]),
                       _ptr(d["topk_ws"]), d["topk_ws"].numel(), self.stream)
             for o, t in zip(out, tmp):
                 o[perm] = t
@@ -510,9 +550,13 @@ def host_bounds(typed: TypedTables) -> Bounds:
 
 
 def build_engine(typed: TypedTables, device=None, tile_w=DEFAULT_TILE_W, timed=False,
-                 denominator="rowsum"):
+                 denominator="rowsum", spgemm="sort", venue_skip=None):
     t0 = time.perf_counter()
-    eng = PathSimEngine(typed, device=device, tile_w=tile_w, denominator=denominator).upload()
+    eng = PathSimEngine(typed, device=device, tile_w=tile_w, denominator=denominator)
+    eng.spgemm = spgemm
+    if venue_skip is not None:
+        eng.venue_skip = bool(venue_skip) and denominator == "rowsum"
+    eng.upload()
     eng.build(timed=timed)
     eng.info.phase_ms["host_total"] = (time.perf_counter() - t0) * 1e3
     return eng

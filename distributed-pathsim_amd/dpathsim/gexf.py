@@ -198,15 +198,19 @@ def _parse_native(path):
         o = off.tolist()
         return [raw[o[i]:o[i + 1]].decode("utf-8") for i in range(k)]
 
-    node_ids = strings(id_buf, id_off, n)
-    labels = strings(lab_buf, lab_off, n)
+    try:
+        node_ids = strings(id_buf, id_off, n)
+        labels = strings(lab_buf, lab_off, n)
+        tvals, rnames = strings(t_buf, t_off, nt), strings(r_buf, r_off, nr)
+    except UnicodeDecodeError:
+        return None      # not UTF-8 after all: the Python loop decodes it as networkx does
     for i in np.flatnonzero(lab_null[:n]).tolist():
         labels[i] = None
     return dict(directed=directed, node_ids=node_ids, labels=labels,
                 node_index=dict(zip(node_ids, range(n))), tcodes=tcodes[:n].astype(np.int64),
-                tvals=strings(t_buf, t_off, nt), src=src[:m].astype(np.int64),
+                tvals=tvals, src=src[:m].astype(np.int64),
                 dst=dst[:m].astype(np.int64), rcodes=rcodes[:m].astype(np.int64),
-                rnames=strings(r_buf, r_off, nr), key=lambda j: _key_at(kbuf, koff, j))
+                rnames=rnames, key=lambda j: _key_at(kbuf, koff, j))
 
 
 def _key_at(buf, off, j):

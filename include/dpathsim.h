@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define DPS_ABI_VERSION 1
+#define DPS_ABI_VERSION 2
 
 enum {
   DPS_OK = 0,
@@ -71,6 +71,17 @@ enum {
 
 int dps_abi_version(void);
 const char* dps_last_error(void);
+
+/* Explicit, process-wide tuning overrides for tests and A/B runs (the library
+ * reads no environment variables; every value 0 = automatic, the default):
+ *   DPS_TUNE_WAVES_PER_ROW  1, 4 or 8 waves share one source row in the hot
+ *                           kernel (automatic: 1 for tile_w <= 8192);
+ *   DPS_TUNE_TILE_BUILD     1 = block-local, 2 = global-atomic C^T tile build
+ *                           (automatic: by the number of mids).
+ * No reference counterpart (Spark picks its own plans). */
+enum { DPS_TUNE_WAVES_PER_ROW = 1, DPS_TUNE_TILE_BUILD = 2, DPS_TUNE_KEYS = 3 };
+int dps_set_tuning(int32_t key, int32_t value);
+int dps_get_tuning(int32_t key);
 /* Number of visible HIP devices (hipGetDeviceCount); < 0 on error. */
 int dps_device_count(void);
 
@@ -271,6 +282,42 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
                        void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Venue skipping for the hot kernel (an exact pruning; no reference
+ * counterpart -- the reference counts every path of the motif,
+ * DPathSim_APVPA.py:90-109).  With the row-sum denominator every target has
+ * g[y] = sum_v C[y,v] s[v] (metapath_global_walk :70-88), so once a
+ * row's top-k is full (k-th score tau) the heavy venues h with
+ * 2 C[x,h] <= tau s[h] cannot lift a target to tau on their own: the kernel
+ * stops scattering their buckets, flags targets from the other venues' counts
+ * with a threshold lowered by max_h C[x,h]/s[h] * g[y], and completes each
+ * flagged target's count exactly from a dense table of C over the heavy venues
+ * before scoring it.  Results are identical with and without it.
+ *
+ * dps_heavy_venues: hv_slot int32[n_mids] = slot in [0, n_hv) of up to n_hv
+ *   venues with the most author entries n_v (dps_walks_fused's n_v), -1 for
+ *   every other venue (and for n_v == 0).  1 <= n_hv <= 64.
+ * dps_heavy_table: hv_c uint16[n_targets * n_hv] (written whole): entry
+ *   label(y) * n_hv + hv_slot[v] = C[y,v] for every author row y < n_targets
+ *   and heavy venue v, 0 elsewhere; label(y) = t_rank[y] (NULL = y).  Needs
+ *   max C <= 65535 (the engine's check).
+ * dps_venue_skip: what the top-k entry points take (host struct, nullable =
+ *   off).  Valid ONLY when their g is the row-sum global walk g = C.s for this
+ *   s (not with the diag denominator); hv_c must use the same t_rank.  Used by
+ *   the W = 8192 kernel; other tile widths ignore it.
+ * ------------------------------------------------------------------------- */
+typedef struct dps_venue_skip {
+  const int64_t* s;          /* s[v] = column sums of C over every AP row (dps_walks_fused) */
+  const int32_t* hv_slot;    /* [n_mids], dps_heavy_venues */
+  const uint16_t* hv_c;      /* [n_targets * n_hv], dps_heavy_table */
+  int32_t n_hv;              /* 1..64 */
+} dps_venue_skip;
+int dps_heavy_venues(const uint32_t* n_v, int64_t n_mids, int32_t n_hv, int32_t* hv_slot,
+                     void* stream);
+int dps_heavy_table(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                    const int32_t* t_rank, int64_t n_targets, const int32_t* hv_slot, int32_t n_hv,
+                    uint16_t* hv_c, void* stream);
+
+/* ---------------------------------------------------------------------------
  * ★ A5+A6+A7 fused: the hot kernel.  For every source row x in
  * [row_begin, row_end) (original author ordinals): M[x,y] = C[x,:].C[y,:] over
  * all targets y != x (metapath_pairwise_walk :90-109), score =
@@ -280,7 +327,8 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
  * score 0.0.  g: original order; g_t/t_perm/t_rank: the relabeling of
  * dps_target_order (all NULL = identity labels, g_t = g); tile_* from
  * dps_ct_tiles_build with the same t_rank (tile_gmin required, tile_maxc
- * optional -- enables skipping tiles that cannot hold a top-k candidate).
+ * optional -- enables skipping tiles that cannot hold a top-k candidate);
+ * vskip: venue skipping (above), NULL = off.
  * Outputs (row-major [row_end-row_begin][k], output row x - row_begin):
  * out_idx int32 (original ordinals), out_cnt int64 (M), out_score double.
  * 1 <= k <= 256.  row_order (nullable, int32[row_end-row_begin]): a
@@ -294,7 +342,7 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
                  const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
                  const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                  const uint32_t* tile_off, const uint32_t* tile_ent,
-                 const uint32_t* tile_maxc, const int64_t* tile_gmin,
+                 const uint32_t* tile_maxc, const int64_t* tile_gmin, const dps_venue_skip* vskip,
                  int64_t row_begin, int64_t row_end, const int32_t* row_order, int32_t k,
                  int32_t* out_idx, int64_t* out_cnt, double* out_score,
                  void* ws, size_t ws_bytes, void* stream);
@@ -307,7 +355,8 @@ int dps_cct_topk_rows(const int64_t* c_ptr, const int32_t* c_col, const int32_t*
                       const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
                       const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                       const uint32_t* tile_off, const uint32_t* tile_ent,
-                      const uint32_t* tile_maxc, const int64_t* tile_gmin, const int32_t* rows,
+                      const uint32_t* tile_maxc, const int64_t* tile_gmin,
+                      const dps_venue_skip* vskip, const int32_t* rows,
                       int64_t n_rows, int32_t k, int32_t* out_idx, int64_t* out_cnt,
                       double* out_score, void* ws, size_t ws_bytes, void* stream);
 
@@ -332,7 +381,8 @@ int dps_cct_topk_split(const int64_t* c_ptr, const int32_t* c_col, const int32_t
                        const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
                        const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                        const uint32_t* tile_off, const uint32_t* tile_ent,
-                       const uint32_t* tile_maxc, const int64_t* tile_gmin, int64_t row_begin,
+                       const uint32_t* tile_maxc, const int64_t* tile_gmin,
+                       const dps_venue_skip* vskip, int64_t row_begin,
                        int64_t row_end, const int32_t* row_order, int64_t n_order,
                        const int32_t* piece_t0, const int32_t* piece_t1, int64_t n_pieces,
                        int32_t* piece_idx, int64_t* piece_cnt, double* piece_score, int32_t k,
@@ -376,6 +426,26 @@ int dps_row_scores(const int64_t* m, const int64_t* g, int64_t gx, int64_t n, do
 int dps_pair_count(const int32_t* a_col, const int32_t* a_val, int64_t a_len,
                    const int32_t* b_col, const int32_t* b_val, int64_t b_len,
                    int64_t* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * RCCL over xGMI: one rank per process and GPU.  Replaces
+ * the Spark shuffle that brings results back to the driver (the .count()
+ * actions DPathSim_APVPA.py:86,107 over the session of :146-168).
+ * dps_comm_get_id: an ncclUniqueId (dps_comm_id_bytes() bytes) on ONE rank;
+ *   the caller shares the bytes with the other ranks out of band.
+ * dps_comm_init: ncclCommInitRank on the CURRENT device (hipSetDevice first);
+ *   *comm_out is opaque.  dps_comm_destroy releases it (NULL is a no-op).
+ * dps_bcast: `bytes` bytes of buf from `root` to every rank (in place).
+ * dps_gather: every rank's `bytes` bytes of send into recv on `root`, rank r
+ *   at recv + r * bytes (recv unused elsewhere).  Device buffers, enqueued on
+ *   the caller's stream like every other entry point.
+ * ------------------------------------------------------------------------- */
+int dps_comm_id_bytes(void);
+int dps_comm_get_id(uint8_t* id_out);
+int dps_comm_init(void** comm_out, int32_t nranks, int32_t rank, const uint8_t* id);
+int dps_comm_destroy(void* comm);
+int dps_bcast(void* comm, void* buf, size_t bytes, int32_t root, void* stream);
+int dps_gather(void* comm, const void* send, void* recv, size_t bytes, int32_t root, void* stream);
 
 /* ---------------------------------------------------------------------------
  * A8. Run-log format (DPathSim_APVPA.py:32-67), host-side, for all-pairs

@@ -41,3 +41,20 @@ def dblp_small_expected():
 def log_triples():
     with open(os.path.join(GOLDEN, "log_triples.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture
+def tune():
+    """Set libdpathsim tuning overrides (dps_set_tuning) for one test; every key
+    set is reset to 0 (automatic) afterwards."""
+    from dpathsim import _lib
+    lib = _lib.load()
+    keys = []
+
+    def _set(key, value):
+        assert lib.dps_set_tuning(key, value) == 0, lib.dps_last_error()
+        keys.append(key)
+
+    yield _set
+    for k in keys:
+        lib.dps_set_tuning(k, 0)

@@ -151,8 +151,9 @@ def _engine_worker(rank, world, port, k, result_path):
         import pathsim_oracle as po
         from dpathsim.engine import build_engine
         from dpathsim.synth import synth_dblp
-        t = synth_dblp(6000, 18000, 300, seed=21).typed()
-        eng = build_engine(t, device="cuda:0", tile_w=1024)
+        from dpathsim.dist import pack_counts
+        t = synth_dblp(30000, 90000, 300, seed=21).typed()
+        eng = build_engine(t, device="cuda:0", tile_w=8192)      # the bench shape
         na = t.n_authors
         bounds = balanced_bounds(eng.row_work(), world)
         r0, r1 = bounds[rank]
@@ -161,11 +162,16 @@ def _engine_worker(rank, world, port, k, result_path):
                     for dt in (torch.int32, torch.int64, torch.float64))
         eng.topk(k, r0, r1, out=tuple(o[: r1 - r0] for o in out))
         res = gather_topk(out, na, world, bounds=bounds)
+        # bench.py's wire path: 8-byte (count, index) words, rescored on rank 0
+        packed = pack_counts(out[0], out[1])
+        res8 = gather_topk_compact(packed, eng.tensor("den")[:na], na, world, bounds=bounds)
         if rank == 0:
             fi, fc, fs = po.COracle.from_typed(t).topk(k, 0, na)
-            gi, gc, gs = (a.cpu().numpy() for a in res)
-            ok = (np.array_equal(gi, fi) and np.array_equal(gc, fc)
-                  and np.array_equal(gs.view(np.int64), fs.view(np.int64)))
+            ok = True
+            for r in (res, res8):
+                gi, gc, gs = (a.cpu().numpy() for a in r)
+                ok = ok and (np.array_equal(gi, fi) and np.array_equal(gc, fc)
+                             and np.array_equal(gs.view(np.int64), fs.view(np.int64)))
             with open(result_path, "w") as f:
                 f.write("ok" if ok else "mismatch")
     finally:
@@ -212,5 +218,48 @@ def _rccl_worker(rank, world, port, k, result_path):
 def test_rccl_compact_gather_one_rank(tmp_path):
     out = tmp_path / "result.txt"
     mp.start_processes(_rccl_worker, args=(1, _free_port(), 10, str(out)), nprocs=1,
+                       join=True, start_method="spawn")
+    assert out.read_text() == "ok"
+
+
+def _rccl_capi_worker(rank, world, port, k, result_path):
+    """The compact gather through libdpathsim's own RCCL communicator
+    (dps_comm_init / dps_gather / dps_bcast; torch.distributed gloo only
+    carries the unique id), one rank -- bench.py's N > 1 wire path."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = None
+    try:
+        import pathsim_oracle as po
+        from dpathsim.dist import RcclComm, pack_counts
+        from dpathsim.engine import build_engine
+        from dpathsim.synth import synth_dblp
+        comm = RcclComm()
+        t = synth_dblp(4000, 12000, 200, seed=8).typed()
+        eng = build_engine(t, device="cuda:0")
+        na = t.n_authors
+        idx, cnt, _ = eng.topk(k)
+        out = torch.empty((na, k), dtype=torch.int64, device="cuda:0")
+        gi, gc, gs = gather_topk_compact(pack_counts(idx, cnt), eng.tensor("den")[:na], na, 1,
+                                         out=out, force_collective=True, comm=comm)
+        fi, fc, fs = po.COracle.from_typed(t).topk(k, 0, na)
+        ok = (np.array_equal(gi.cpu().numpy(), fi) and np.array_equal(gc.cpu().numpy(), fc)
+              and np.array_equal(gs.cpu().numpy().view(np.int64), fs.view(np.int64)))
+        b = torch.arange(1000, dtype=torch.int64, device="cuda:0")
+        comm.bcast(b)
+        ok = ok and bool((b.cpu() == torch.arange(1000)).all())
+        with open(result_path, "w") as f:
+            f.write("ok" if ok else "mismatch")
+    finally:
+        if comm is not None:
+            comm.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_capi_compact_gather_one_rank(tmp_path):
+    out = tmp_path / "result.txt"
+    mp.start_processes(_rccl_capi_worker, args=(1, _free_port(), 10, str(out)), nprocs=1,
                        join=True, start_method="spawn")
     assert out.read_text() == "ok"

@@ -154,13 +154,12 @@ def test_topk_rows_matches_contiguous_launch():
 
 
 @pytest.mark.parametrize("multi,spgemm", [(1, "sort"), (3, "sort"), (3, "hash")])
-def test_spgemm_long_and_huge_rows(multi, spgemm, monkeypatch):
+def test_spgemm_long_and_huge_rows(multi, spgemm):
     """Rows of every length class, papers of 1 (single-mid path) or up to 3
     venues each (repeats dropped by the PX distinct), through the multi-mid
     SpGEMMs: expand + segmented sort/unique (the default) and the hash SpGEMM
     (lane L <= 16, LDS hash 16 < L <= 4096, global-scratch sort L > 4096) --
     C, g and the top-k against the oracle."""
-    monkeypatch.setenv("DPATHSIM_SPGEMM", spgemm)
     import pathsim_oracle as po
     from dpathsim.engine import build_engine
     from dpathsim.graph import Graph
@@ -186,7 +185,7 @@ def test_spgemm_long_and_huge_rows(multi, spgemm, monkeypatch):
     g = Graph(types, ["author", "paper", "venue"], np.array(src), np.array(dst), rel,
               ["author_of", "submit_at"], node_ids=lambda i: f"n{i}", labels=lambda i: f"L{i}")
     t = g.typed()
-    eng = build_engine(t, tile_w=1024)
+    eng = build_engine(t, tile_w=1024, spgemm=spgemm)
     co = po.COracle.from_typed(t)
     cp, cc, cv, s, gg = co.export()
     nnz = eng.info.nnz_c

@@ -41,12 +41,13 @@ def test_synth_20k_top10(tile_w):
 
 
 @pytest.mark.parametrize("tile_w,nw", [(8192, 1), (8192, 4), (4096, 4), (16384, 1), (32768, 1)])
-def test_synth_20k_waves_per_row(tile_w, nw, monkeypatch):
+def test_synth_20k_waves_per_row(tile_w, nw, tune):
     """Both kernel shapes -- one wave per row and a workgroup per row
-    (DPATHSIM_NW overrides the tile-width default) -- give the oracle's top-k."""
+    (dps_set_tuning overrides the tile-width default) -- give the oracle's top-k."""
+    from dpathsim import _lib
     from dpathsim.engine import build_engine
     from dpathsim.synth import synth_dblp
-    monkeypatch.setenv("DPATHSIM_NW", str(nw))
+    tune(_lib.TUNE_WAVES_PER_ROW, nw)
     t = synth_dblp(20_000, 60_000, 500, seed=7).typed()
     _check(build_engine(t, tile_w=tile_w), _oracle(t), 10)
     _check(build_engine(t, tile_w=tile_w), _oracle(t), 100, rows=(0, 3000))
@@ -83,11 +84,12 @@ def test_aptpa_multi_topic():
 
 
 @pytest.mark.parametrize("tile_w,glob", [(256, "0"), (1024, "0"), (8192, "0"), (8192, "1")])
-def test_many_mids_tile_build(tile_w, glob, monkeypatch):
+def test_many_mids_tile_build(tile_w, glob, tune):
     """More mids than one block's LDS counters (20,000 venues > 8192): the
     block-local tile build with one block per mid range (default) and the
-    global-atomic build (DPATHSIM_TILE_GLOBAL=1) against the oracle."""
-    monkeypatch.setenv("DPATHSIM_TILE_GLOBAL", glob)
+    global-atomic build (dps_set_tuning TILE_BUILD = 2) against the oracle."""
+    from dpathsim import _lib
+    tune(_lib.TUNE_TILE_BUILD, 2 if glob == "1" else 0)
     from dpathsim.engine import build_engine
     from dpathsim.synth import synth_dblp
     t = synth_dblp(6_000, 24_000, 20_000, seed=29).typed()

@@ -1,5 +1,6 @@
 """CPU: host logic of the product package (loader, typed tables, generator, C ABI)."""
 import ctypes
+import ctypes as C
 import os
 import re
 
@@ -24,7 +25,7 @@ def test_header_symbols_exported():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(_lib.exported_symbols()) == declared
-    assert lib.dps_abi_version() == 1
+    assert lib.dps_abi_version() == 2
 
 
 def test_no_cpu_fallback_when_library_missing(monkeypatch):
@@ -173,13 +174,49 @@ def test_c_abi_rejects_bad_arguments_without_gpu():
     """Argument validation happens host-side before any HIP call."""
     lib = _lib.load()
     rc = lib.dps_cct_topk(None, None, None, None, None, None, None, 10, 5, 300, None, None,
-                          None, None, 0, 10, None, 10, None, None, None, None, 0, None)
+                          None, None, None, 0, 10, None, 10, None, None, None, None, 0, None)
     assert rc == _lib.DPS_ERR_UNSUPPORTED     # tile_w 300 is not a power of two
     assert b"tile_w" in lib.dps_last_error()
     rc = lib.dps_cct_topk(None, None, None, None, None, None, None, 10, 5, 256, None, None,
-                          None, None, 0, 10, None, 0, None, None, None, None, 0, None)
+                          None, None, None, 0, 10, None, 0, None, None, None, None, 0, None)
     assert rc == _lib.DPS_ERR_UNSUPPORTED     # k = 0
     assert lib.dps_csr_build_workspace_size(100, 10) > 0
+    # venue skipping: the struct's table width and pointers are validated too
+    ws = C.create_string_buffer(512)
+    ws_al = (C.addressof(ws) + 255) // 256 * 256
+    vs = _lib.VenueSkip(1, 1, 1, 65)
+    rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 256, 8, 8, None, 8,
+                          C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 256, None)
+    assert rc == _lib.DPS_ERR_INVALID and b"n_hv" in lib.dps_last_error()
+    vs = _lib.VenueSkip(None, 1, 1, 32)
+    rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 256, 8, 8, None, 8,
+                          C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 256, None)
+    assert rc == _lib.DPS_ERR_INVALID and b"dps_venue_skip" in lib.dps_last_error()
+    assert lib.dps_heavy_venues(None, 10, 0, None, None) == _lib.DPS_ERR_INVALID
+    assert lib.dps_heavy_table(None, None, None, None, 10, None, 65, None, None) == _lib.DPS_ERR_INVALID
+
+
+def test_tuning_overrides():
+    """dps_set_tuning: explicit overrides replace environment variables (the
+    default library reads none); bad keys and values are rejected."""
+    lib = _lib.load()
+    assert lib.dps_get_tuning(_lib.TUNE_WAVES_PER_ROW) == 0
+    assert lib.dps_set_tuning(_lib.TUNE_WAVES_PER_ROW, 3) == _lib.DPS_ERR_INVALID
+    assert lib.dps_set_tuning(99, 1) == _lib.DPS_ERR_INVALID
+    assert lib.dps_set_tuning(_lib.TUNE_TILE_BUILD, 3) == _lib.DPS_ERR_INVALID
+    try:
+        assert lib.dps_set_tuning(_lib.TUNE_WAVES_PER_ROW, 4) == 0
+        assert lib.dps_get_tuning(_lib.TUNE_WAVES_PER_ROW) == 4
+    finally:
+        lib.dps_set_tuning(_lib.TUNE_WAVES_PER_ROW, 0)
+    assert lib.dps_get_tuning(_lib.TUNE_WAVES_PER_ROW) == 0
+
+
+def test_library_reads_no_environment_knobs():
+    """The production library carries no DPATHSIM_* environment names: a stray
+    shell variable cannot change what it computes or how fast."""
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"DPATHSIM_" not in data
 
 
 def _raw_truth(typed):
@@ -281,6 +318,22 @@ def test_native_gexf_scan_equals_python_loop(tmp_path, case):
     assert a.type_names == b.type_names and a.rel_names == b.rel_names
     v, e = _nx_tuples(str(p))
     assert a.vertices() == v and a.edges() == e
+
+
+def test_native_gexf_declines_latin1(tmp_path):
+    """An ISO-8859-1 file with non-ASCII names: the native scanner declines it
+    (declared encoding) and the Python loop decodes it as networkx does."""
+    text = _NATIVE_CASES["edge_only_node_typed_later"].replace(
+        '<?xml version="1.0"?>', '<?xml version="1.0" encoding="ISO-8859-1"?>').replace(
+        'label="X"', 'label="J\u00fcrgen M\u00fcller"')
+    p = tmp_path / "latin1.gexf"
+    p.write_bytes(text.encode("latin-1"))
+    with pytest.raises(RuntimeError):
+        read_gexf(str(p), native=True)
+    a = read_gexf(str(p))
+    v, e = _nx_tuples(str(p))
+    assert a.vertices() == v and a.edges() == e
+    assert "J\u00fcrgen M\u00fcller" in [x[1] for x in a.vertices()]
 
 
 def test_native_gexf_scan_synthetic_and_fallbacks(tmp_path):
