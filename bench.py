@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--config", default="config3")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink authors/papers (debug)")
     ap.add_argument("--k", type=int, default=None)
-    ap.add_argument("--tile-w", type=int, default=8192)
+    ap.add_argument("--tile-w", type=int, default=16384)
     ap.add_argument("--denominator", default="rowsum", choices=["rowsum", "diag"])
     ap.add_argument("--venue-skip", type=int, default=None,
                     help="1/0: force venue skipping on/off (default: the engine's)")
@@ -313,7 +313,7 @@ def main():
                        "parallelism": f"row-shard x{world} (work-balanced, heaviest rows first)"},
             # bound: the busiest resource per the HEAD counters (LDS array; the
             # kernel is latency-bound at the occupancy its LDS allows)
-            "roofline": {"bound": "lds", "kernel": "dps_cct_topk (k_cct1, W 8192)",
+            "roofline": {"bound": "lds", "kernel": f"dps_cct_topk (k_cct1, W {args.tile_w})",
                          "achieved": lds_achieved, "peak": LDS_PEAK_GBS,
                          "unit": "GB/s (ds_read_b128-equivalent)",
                          "frac": lds_achieved / LDS_PEAK_GBS if lds_achieved else None,
@@ -323,7 +323,8 @@ def main():
                          "lds_floor_ms_by_class": lds_floor_ms,
                          "lds_floor_ms": sum(lds_floor_ms.values()),
                          "passes": n_pass, "chunks": n_chunk, "verified": n_ver,
-                         "venue_skip": eng._vskip is not None,
+                         "venue_skip": bool(eng._ext is not None and eng._ext.s),
+                         "half_tiles": bool(eng._ext is not None and eng._ext.half_ent),
                          "avg_launch_ms": topk_ms,
                          "pmc": pmc,
                          "hbm": {"algorithmic_bytes": bytes_launch,

@@ -597,7 +597,7 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
                          const int32_t* t_rank, int64_t n_targets, int64_t n_mids,
                          int32_t tile_w, const uint32_t* tile_off, const uint32_t* tile_ent,
                          const uint32_t* tile_maxc, const int64_t* tile_gmin,
-                         const dps_venue_skip* vskip, int64_t row_begin,
+                         const dps_cct_ext* ext, int64_t row_begin,
                          int64_t n_rows, const int32_t* row_order, bool out_by_slot, int32_t k,
                          int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
                          size_t ws_bytes, void* stream, int64_t n_pieces = 0,
@@ -616,19 +616,30 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
               "g, tile_off, tile_ent and tile_gmin are required");
   DPS_REQUIRE(ws && ws_bytes >= dps_cct_topk_workspace_size(), DPS_ERR_WORKSPACE,
               "cct_topk workspace too small");
+  const bool vskip = ext && ext->s;
   if (vskip) {
-    DPS_REQUIRE(vskip->s && vskip->hv_slot && vskip->hv_c, DPS_ERR_INVALID,
-                "dps_venue_skip needs s, hv_slot and hv_c");
-    DPS_REQUIRE(vskip->n_hv >= 1 && vskip->n_hv <= 64, DPS_ERR_INVALID,
-                "dps_venue_skip.n_hv must be in [1, 64], got %d", vskip->n_hv);
+    DPS_REQUIRE(ext->hv_slot && ext->hv_c, DPS_ERR_INVALID,
+                "dps_cct_ext venue skipping needs s, hv_slot and hv_c");
+    DPS_REQUIRE(ext->n_hv >= 1 && ext->n_hv <= 64, DPS_ERR_INVALID,
+                "dps_cct_ext.n_hv must be in [1, 64], got %d", ext->n_hv);
+  }
+  const bool half = ext && ext->half_ent;
+  if (half) {
+    DPS_REQUIRE(shift == 14, DPS_ERR_INVALID, "companion u8 tiles need tile_w 16384");
+    DPS_REQUIRE(ext->half_off && (ext->half_maxc || !tile_maxc), DPS_ERR_INVALID,
+                "dps_cct_ext companion tiles need half_off (and half_maxc with tile_maxc)");
   }
   auto st = static_cast<hipStream_t>(stream);
   if (n_rows == 0) return DPS_OK;
   CctParams p;
-  p.s = vskip ? vskip->s : nullptr;
-  p.hv_slot = vskip ? vskip->hv_slot : nullptr;
-  p.hv_c = vskip ? vskip->hv_c : nullptr;
-  p.n_hv = vskip ? vskip->n_hv : 0;
+  p.s = vskip ? ext->s : nullptr;
+  p.hv_slot = vskip ? ext->hv_slot : nullptr;
+  p.hv_c = vskip ? ext->hv_c : nullptr;
+  p.n_hv = vskip ? ext->n_hv : 0;
+  p.h_off = half ? ext->half_off : nullptr;
+  p.h_ent = half ? ext->half_ent : nullptr;
+  p.h_maxc = half ? (tile_maxc ? ext->half_maxc : ext->half_off) : nullptr;
+  p.T8 = (n_targets + 8191) / 8192;
   p.c_ptr = c_ptr; p.c_col = c_col; p.c_val = c_val;
   p.g = g; p.g_t = g_t ? g_t : g; p.t_perm = t_perm; p.t_rank = t_rank;
   p.tile_off = tile_off; p.tile_ent = tile_ent; p.tile_gmin = tile_gmin;
@@ -640,13 +651,16 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   // waves per row: one wave owns a row for W <= 8192 (8 KB of u8 accumulators,
   // no barriers, one exact running top-k per row); wider tiles share a row
   // between the waves of a workgroup (4 x 32 KB or 2 x 64 KB per CU)
-  int nw = shift <= 13 ? 1 : shift == 16 ? 8 : 4;
+  // (W = 16384 holds 4-bit-counter entries, which only the lean kernel reads)
+  int nw = shift <= 14 ? 1 : shift == 16 ? 8 : 4;
   if (const int t = tuning(DPS_TUNE_WAVES_PER_ROW)) nw = t;
 #ifdef DPS_PROFILE
   if (const char* e = std::getenv("DPATHSIM_NW")) nw = std::atoi(e);   // experiments
 #endif
   DPS_REQUIRE(nw == 1 || nw == 4 || nw == 8, DPS_ERR_INVALID, "waves per row must be 1, 4 or 8");
-  DPS_REQUIRE(nw != 8 || shift > 13, DPS_ERR_INVALID, "8 waves per row need tile_w >= 16384");
+  DPS_REQUIRE(nw != 8 || shift > 14, DPS_ERR_INVALID, "8 waves per row need tile_w >= 32768");
+  DPS_REQUIRE(nw == 1 || shift != 14, DPS_ERR_UNSUPPORTED,
+              "tile_w 16384 (4-bit counter entries) runs one wave per row");
 
   p.dbuf = nw > 1 && shift <= 14;   // 2 x W bytes of u8 accumulators up to W = 16384, one 32 KB buffer above
   p.row_begin = row_begin; p.row_order = row_order; p.out_by_slot = out_by_slot;
@@ -665,11 +679,11 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : 4 * sizeof(unsigned long long), st));
   // the bench shape (W = 8192, one wave per row) runs the lean kernel
   // (dps_cct1.hip); DPATHSIM_LEAN=0 selects this file's general kernel
-  bool lean = shift == 13 && nw == 1 && (p.ablate == 0 || p.ablate == 16);
+  bool lean = (shift == 13 || shift == 14) && nw == 1 && (p.ablate == 0 || p.ablate == 16);
 #ifdef DPS_PROFILE
   if (const char* e = std::getenv("DPATHSIM_LEAN")) lean = lean && std::atoi(e) != 0;   // experiments
 #endif
-  if (lean) return cct1_launch(p, st);
+  if (lean || shift == 14) return cct1_launch(p, st);
   if (shift <= 13) return dispatch<true>(p, nw, k, st);   // 16-bit tile entries
   return dispatch<false>(p, nw, k, st);
 }
@@ -678,7 +692,7 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
                  const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
                  const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                  const uint32_t* tile_off, const uint32_t* tile_ent, const uint32_t* tile_maxc,
-                 const int64_t* tile_gmin, const dps_venue_skip* vskip, int64_t row_begin,
+                 const int64_t* tile_gmin, const dps_cct_ext* ext, int64_t row_begin,
                  int64_t row_end, const int32_t* row_order, int32_t k,
                  int32_t* out_idx, int64_t* out_cnt, double* out_score, void* ws,
                  size_t ws_bytes, void* stream) {
@@ -686,7 +700,7 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
               "row range [%lld, %lld) outside [0, %lld)", static_cast<long long>(row_begin),
               static_cast<long long>(row_end), static_cast<long long>(n_targets));
   return cct_topk_impl(c_ptr, c_col, c_val, g, g_t, t_perm, t_rank, n_targets, n_mids, tile_w,
-                       tile_off, tile_ent, tile_maxc, tile_gmin, vskip, row_begin,
+                       tile_off, tile_ent, tile_maxc, tile_gmin, ext, row_begin,
                        row_end - row_begin, row_order, false, k, out_idx, out_cnt, out_score, ws, ws_bytes, stream);
 }
 
@@ -695,14 +709,14 @@ int dps_cct_topk_rows(const int64_t* c_ptr, const int32_t* c_col, const int32_t*
                       const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                       const uint32_t* tile_off, const uint32_t* tile_ent,
                       const uint32_t* tile_maxc, const int64_t* tile_gmin,
-                      const dps_venue_skip* vskip, const int32_t* rows,
+                      const dps_cct_ext* ext, const int32_t* rows,
                       int64_t n_rows, int32_t k, int32_t* out_idx, int64_t* out_cnt,
                       double* out_score, void* ws, size_t ws_bytes, void* stream) {
   DPS_REQUIRE(n_rows >= 0 && n_rows <= n_targets, DPS_ERR_INVALID, "bad n_rows %lld",
               static_cast<long long>(n_rows));
   DPS_REQUIRE(n_rows == 0 || rows, DPS_ERR_INVALID, "rows is required");
   return cct_topk_impl(c_ptr, c_col, c_val, g, g_t, t_perm, t_rank, n_targets, n_mids, tile_w,
-                       tile_off, tile_ent, tile_maxc, tile_gmin, vskip, 0, n_rows, rows, true, k,
+                       tile_off, tile_ent, tile_maxc, tile_gmin, ext, 0, n_rows, rows, true, k,
                        out_idx, out_cnt, out_score, ws, ws_bytes, stream);
 }
 
@@ -711,7 +725,7 @@ int dps_cct_topk_split(const int64_t* c_ptr, const int32_t* c_col, const int32_t
                        const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                        const uint32_t* tile_off, const uint32_t* tile_ent,
                        const uint32_t* tile_maxc, const int64_t* tile_gmin,
-                       const dps_venue_skip* vskip, int64_t row_begin,
+                       const dps_cct_ext* ext, int64_t row_begin,
                        int64_t row_end, const int32_t* row_order, int64_t n_order,
                        const int32_t* piece_t0, const int32_t* piece_t1, int64_t n_pieces,
                        int32_t* piece_idx, int64_t* piece_cnt, double* piece_score, int32_t k,
@@ -727,7 +741,7 @@ int dps_cct_topk_split(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   DPS_REQUIRE(n_pieces == 0 || (piece_t0 && piece_t1 && piece_idx && piece_cnt && piece_score),
               DPS_ERR_INVALID, "piece ranges and outputs are required");
   return cct_topk_impl(c_ptr, c_col, c_val, g, g_t, t_perm, t_rank, n_targets, n_mids, tile_w,
-                       tile_off, tile_ent, tile_maxc, tile_gmin, vskip, row_begin, n_order,
+                       tile_off, tile_ent, tile_maxc, tile_gmin, ext, row_begin, n_order,
                        row_order, false, k, out_idx, out_cnt, out_score, ws, ws_bytes, stream, n_pieces,
                        piece_t0, piece_t1, piece_idx, piece_cnt, piece_score);
 }

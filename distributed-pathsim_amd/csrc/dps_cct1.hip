@@ -50,11 +50,32 @@
 namespace dps {
 namespace {
 
-constexpr int kS1 = 13;                       // log2 W
-constexpr int kW1 = 1 << kS1;                 // 8192 targets per tile
-constexpr int kAcc1 = kW1 / 4;                // accumulator dwords (packed u8)
-constexpr int kSeg1 = 10;                     // threshold segments of 1024 targets
-constexpr uint32_t kLabMask1 = (kW1 - 1) & ~3u;
+// Two tile formats share this kernel (template F, dps_tiles.hip):
+//   F = 1  W = 8192 targets, 16-bit entries (l << 3) | e, packed u8 counters;
+//   F = 2  W = 16384 targets, 16-bit entries (l << 2) | e, packed 4-bit counters.
+// Both keep one tile's counters in 8 KiB of LDS per wave (2048 dwords), and in
+// both the entry's low five bits are the add's shift and (entry >> 3) masked
+// to a dword is its LDS byte address, so the scatter is the same code.  The
+// 4-bit counters halve the accumulator passes per row.  A tile whose bound
+// exceeds 15 runs as its two halves from a companion W = 8192 (u8) tile set
+// when the caller provides one ("dual", p.h_ent): each half scatters only its
+// own entries, through the same branch-free path; without it the tile takes
+// wide 4-bit passes (u8 / u16 / u32 counters, one entry at a time).
+constexpr int kAcc1 = 2048;                   // accumulator dwords (8 KiB)
+constexpr uint32_t kLabMask1 = 0x1FFCu;       // (entry >> 3) & mask = dword byte address
+template <int F> struct Fmt;
+template <> struct Fmt<1> {
+  static constexpr int S = 13;                // log2 W
+  static constexpr int SEG = 10;              // threshold segments of 1024 targets
+  static constexpr int BITS = 8;              // counter bits of the base pass
+  static constexpr uint32_t UB0 = 0xFFu;      // largest bound of the base pass
+};
+template <> struct Fmt<2> {
+  static constexpr int S = 14;
+  static constexpr int SEG = 11;              // 2048 targets: one 64-lane x 16 B block
+  static constexpr int BITS = 4;
+  static constexpr uint32_t UB0 = 0xFu;
+};
 #ifndef DPS_EPI1
 #define DPS_EPI1 2
 #endif
@@ -134,25 +155,34 @@ __device__ __forceinline__ int next_tile(const CctParams& p, Win1& w, int t_end,
 // Bucket bounds of one tile (lane j < 64: venue j) and the smallest g of each of
 // its 8 threshold segments (lane s < 8), loaded one stage ahead.
 struct Pend1 {
-  int t;
+  int t;         // tile (u8h: a half tile of the companion W = 8192 set)
   uint32_t ub;
+  bool u8h;
   uint32_t lo, hi;
+  uint32_t mx;   // venue skipping: max C[y,v] over the tile's targets (lane = venue)
   int64_t gs;
 };
 
-__device__ __forceinline__ void pend_load(const CctParams& p, Pend1& P, int t, uint32_t ub, int d0,
-                                          uint32_t vT, int lane) {
+template <int F, bool HV>
+__device__ __forceinline__ void pend_load(const CctParams& p, Pend1& P, int t, uint32_t ub, bool u8h,
+                                          int d0, uint32_t vT, uint32_t vT8, int lane) {
   P.t = t;
   P.ub = ub;
+  P.u8h = u8h;
   P.lo = P.hi = 0;
+  P.mx = 0;
   P.gs = 0;
   if (t < 0) return;
   if (lane < d0) {
-    P.lo = p.tile_off[vT + static_cast<uint32_t>(t)];
-    P.hi = p.tile_off[vT + static_cast<uint32_t>(t) + 1u];
+    const uint32_t* off = u8h ? p.h_off : p.tile_off;
+    const uint32_t b = (u8h ? vT8 : vT) + static_cast<uint32_t>(t);
+    P.lo = off[b];
+    P.hi = off[b + 1u];
+    if (HV) P.mx = p.use_bounds ? (u8h ? p.h_maxc : p.tile_maxc)[b] : 0xFFFFu;
   }
-  if (lane < (kW1 >> kSeg1)) {
-    const int64_t i = (static_cast<int64_t>(t) << kS1) + (static_cast<int64_t>(lane) << kSeg1);
+  if (lane < 8) {
+    const int sh = u8h ? Fmt<1>::S : Fmt<F>::S, sg = u8h ? Fmt<1>::SEG : Fmt<F>::SEG;
+    const int64_t i = (static_cast<int64_t>(t) << sh) + (static_cast<int64_t>(lane) << sg);
     P.gs = p.g_t[i < p.n_targets ? i : p.n_targets - 1];
   }
 }
@@ -160,16 +190,29 @@ __device__ __forceinline__ void pend_load(const CctParams& p, Pend1& P, int t, u
 struct Stage1 {
   Stage S;       // chunk group, tile, pass mode (shared helpers' view)
   float gsf;     // lane s < 8: smallest g of segment s, as float
+  bool u8h;      // a u8 half tile of the companion set (F = 2, dual)
+  int ubh;       // venue skipping: sum_{h in H} C[x,h] * maxc[h, tile] >= M_H of any target
 };
 
 // hm: the venue lanes (H) whose buckets this stage skips (venue skipping).
+template <int F>
 __device__ __forceinline__ void stage_make(Stage1& X, const Pend1& P, int c, int d0, uint64_t hm,
                                            int lane) {
   X.S.t = P.t;
-  X.S.lnp = P.ub <= 0xFFu ? 0 : P.ub <= 0xFFFFu ? 1 : 2;
+  X.u8h = P.u8h;
+  // log2 of the passes: counters of BITS << lnp bits must hold the bound
+  if (F == 1 || P.u8h) X.S.lnp = P.ub <= 0xFFu ? 0 : P.ub <= 0xFFFFu ? 1 : 2;
+  else X.S.lnp = P.ub <= 0xFu ? 0 : P.ub <= 0xFFu ? 1 : P.ub <= 0xFFFFu ? 2 : 3;
   X.S.pass = 0;
   const bool skip = (hm >> lane) & 1ull;          // an H venue's bucket is not scattered
   grp_set(X.S.G, P.lo, skip ? P.lo : P.hi, c, d0);
+  X.ubh = 0;
+  if (hm) {
+    // c, mx <= 65535: the product fits 32 bits; a product beyond 16 bits makes
+    // the bound useless (saturate upward: a larger ubh is always sound)
+    const uint32_t pr = skip ? static_cast<uint32_t>(c) * P.mx : 0u;
+    X.ubh = ballot(pr > 0xFFFFu) ? 0x3FFFFFFF : static_cast<int>(wave_sum_u32(pr));
+  }
   X.S.nb = (X.S.G.nq + kWave * kU - 1) / (kWave * kU);
   X.S.gq = 0;
   X.gsf = i64_f32(P.gs);
@@ -281,14 +324,16 @@ __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& t
 // u16 / u32 pass epilogue (UB > 255, rare): scan + zero the accumulator of
 // pass `pass` (2 or 1 targets per dword), queue targets reaching their
 // segment's threshold.
-template <int KPL, bool HV>
+template <int F, int KPL, bool HV>
 __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                           const Stage& S, int lane, int64_t x_lab, int64_t gx,
                                           int mseg, int c, uint32_t hv, uint64_t hm, uint32_t& nver) {
+  constexpr int kS1 = Fmt<F>::S, kSeg1 = Fmt<F>::SEG;
   const int lnp = S.lnp;
-  const int tpd_shift = 2 - lnp;                     // log2(targets per dword)
-  const int bits = 8 << lnp;
-  const uint32_t vmask = lnp == 2 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
+  const int bits = Fmt<F>::BITS << lnp;              // 8..32
+  const int tpd_shift = (F == 1 ? 2 : 3) - lnp;      // log2(targets per dword)
+  const uint32_t vmask = bits == 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
+  const int blnp = bits == 8 ? 0 : bits == 16 ? 1 : 2;   // block_any's counter width
   const int64_t tile_base = S.t << kS1;
   const int pass_base = S.pass << (kS1 - lnp);
   for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4) {
@@ -297,10 +342,10 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
     *reinterpret_cast<uint4*>(acc + b) = make_uint4(0, 0, 0, 0);
     const int i0 = pass_base + (b << tpd_shift);     // first target of this lane's 16 bytes
     const uint32_t m = static_cast<uint32_t>(__shfl(mseg, (i0 >> kSeg1) & (kWave - 1), kWave));
-    const bool any = block_any(a, m, lnp);
+    const bool any = block_any(a, m, blnp);
     if (!ballot(any)) continue;
 #pragma unroll 1
-    for (int v = 0; v < (16 >> lnp); ++v) {
+    for (int v = 0; v < (128 / bits); ++v) {
       const int di = v >> tpd_shift;
       const uint32_t wv = di == 0 ? a.x : di == 1 ? a.y : di == 2 ? a.z : a.w;
       const uint32_t M = (wv >> ((v & ((1 << tpd_shift) - 1)) * bits)) & vmask;
@@ -314,6 +359,107 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
   }
 }
 
+// Per-nibble flags (bit 3) of a packed 4-bit dword: nibble >= m, 1 <= m <= 15
+// (no carry leaves a nibble: low3 + 16 - m <= 14).
+__device__ __forceinline__ uint32_t ge_u4(uint32_t a, uint32_t m) {
+  const uint32_t lo = a & 0x77777777u;
+  if (m <= 8u) return (a | (lo + (8u - m) * 0x11111111u)) & 0x88888888u;
+  return (a & (lo + (16u - m) * 0x11111111u)) & 0x88888888u;
+}
+
+// 4-bit epilogue over the whole W = 16384 tile: 8 blocks of 2048 targets (one
+// threshold segment each; lane l reads dwords 4l..4l+3 of the block = targets
+// 32l..32l+31), read and zeroed kEpi1 at a time; candidates queued as in epi1_u8.
+template <int KPL, bool HV>
+__device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
+                                        int t, int lane, int64_t x_lab, int64_t gx, int mseg,
+                                        int c, uint32_t hv, uint64_t hm, uint32_t& nver) {
+  constexpr int kS = Fmt<2>::S, kSeg = Fmt<2>::SEG;
+  const int64_t tile_base = static_cast<int64_t>(t) << kS;
+  const int64_t xr = x_lab - tile_base;
+  const bool xin = xr >= 0 && xr < (int64_t(1) << kS);   // the source is a target of this tile
+  const int xrel = xin ? static_cast<int>(xr) : 0;
+  auto block = [&](uint4 a, int blk) {
+    const uint32_t m = static_cast<uint32_t>(readlane(mseg, blk));
+    if (m > 15u) return;                           // no 4-bit count reaches m
+    const uint32_t pm = (0x10u - (0x80000000u >> __builtin_clz(m))) * 0x11111111u;
+    if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) return;
+    // target (8*dw + nib) of this lane's 32 -> bit 4*nib + 3 - dw
+    uint32_t F4 = ge_u4(a.x, m) | (ge_u4(a.y, m) >> 1) | (ge_u4(a.z, m) >> 2) | (ge_u4(a.w, m) >> 3);
+    const int i0 = (blk << kSeg) + (lane << 5);
+    if (xin) {                                     // the source itself never counts
+      const int rel = xrel - i0;
+      if (rel >= 0 && rel < 32) F4 &= ~(1u << ((rel & 7) * 4 + 3 - (rel >> 3)));
+    }
+    if (!ballot(F4 != 0)) return;
+    for (;;) {
+      const bool has = F4 != 0;
+      const uint64_t mk = ballot(has);
+      if (!mk) break;
+      int lab = 0, mv = 0;
+      if (has) {
+        const int bit = __builtin_ctz(F4);
+        F4 &= F4 - 1;
+        const int nib = bit >> 2, dw = 3 - (bit & 3);
+        const uint32_t w01 = (dw & 1) ? a.y : a.x;
+        const uint32_t w23 = (dw & 1) ? a.w : a.z;
+        const uint32_t wv = (dw & 2) ? w23 : w01;
+        lab = static_cast<int>(tile_base + i0 + dw * 8 + nib);
+        mv = static_cast<int>((wv >> (nib * 4)) & 0xFu);
+      }
+      vq_push(Q, has, lab, mv, mk, lane);
+      if (Q.n >= kWave) vq_flush<KPL, HV>(p, Q, top, kWave, gx, lane, c, hv, hm, nver);
+    }
+  };
+#pragma unroll 1
+  for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4 * kEpi1) {
+    uint4 a[kEpi1];
+#pragma unroll
+    for (int i = 0; i < kEpi1; ++i)
+      a[i] = *reinterpret_cast<const uint4*>(acc + b0 + i * kWave * 4 + lane * 4);
+#pragma unroll
+    for (int i = 0; i < kEpi1; ++i)
+      *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < kEpi1; ++i) block(a[i], (b0 >> 8) + i);
+  }
+}
+
+// Wide passes of the 4-bit format (lnp 1..3: u8 / u16 / u32 counters over a
+// half / quarter / eighth of the tile per pass), one entry at a time; padding
+// codes (e >= 2 at l % 8 == 7) add nothing.
+__device__ __forceinline__ void acc_add4(uint32_t* acc, uint32_t h, int c, int lnp, int pass) {
+  const uint32_t e = h & 3u, yl = h >> 2;
+  if ((yl & 7u) == 7u && e >= 2u) return;
+  if (static_cast<int>(yl >> (14 - lnp)) != pass) return;
+  const uint32_t local = yl & ((1u << (14 - lnp)) - 1u);
+  const int bits = 4 << lnp;
+  const int tpds = 3 - lnp;                          // log2(targets per dword)
+  const uint32_t val = static_cast<uint32_t>(c) << e;
+  const uint32_t add = val << ((local & ((1u << tpds) - 1u)) * bits);
+  __hip_atomic_fetch_add(acc + (local >> tpds), add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// A batch into the accumulator: the base pass by the shared branch-free u8 /
+// 4-bit path, wide passes entry by entry (u8h: u8-format entries).
+template <int F>
+__device__ __forceinline__ void scatter_f(const Batch& B, const Stage& S, uint32_t* acc, bool u8h) {
+  if (F == 1 || u8h || S.lnp == 0) {
+    scatter_any<true>(B, S, acc, 0u, kLabMask1, Fmt<1>::S);
+    return;
+  }
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    if (B.c[u] == 0) continue;
+    const uint32_t w4[4] = {B.e[u].x, B.e[u].y, B.e[u].z, B.e[u].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc_add4(acc, w4[q] & 0xFFFFu, B.c[u], S.lnp, S.pass);
+      acc_add4(acc, w4[q] >> 16, B.c[u], S.lnp, S.pass);
+    }
+  }
+}
+
 // u8 epilogue over the whole tile: 8 blocks of 1024 targets (one threshold
 // segment each, lane l reads dwords 4l..4l+3 of the block), read and zeroed 4
 // at a time; candidates are queued and scored 64 at a time by flush().
@@ -321,6 +467,8 @@ template <int KPL, bool HV>
 __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                         int t, int lane, int64_t x_lab, int64_t gx, int mseg,
                                         int c, uint32_t hv, uint64_t hm, uint32_t& nver) {
+  constexpr int kS1 = Fmt<1>::S, kSeg1 = Fmt<1>::SEG;
+  constexpr int kW1 = 1 << kS1;
   const int64_t tile_base = static_cast<int64_t>(t) << kS1;
   const int64_t xr = x_lab - tile_base;
   const bool xin = xr >= 0 && xr < kW1;          // the source is a target of this tile
@@ -434,18 +582,21 @@ __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __
 
 // Venues 64.. of a row with more than 64 venues: their buckets of tile t,
 // loaded and scattered synchronously (pass `pass` of mode lnp).
+template <int F>
 __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, uint32_t* acc,
-                                            int64_t pb, int d, int lane) {
+                                            int64_t pb, int d, int lane, bool u8h) {
+  const uint32_t* off = u8h ? p.h_off : p.tile_off;
+  const uint32_t* ent = u8h ? p.h_ent : p.tile_ent;
+  const uint32_t T = static_cast<uint32_t>(u8h ? p.T8 : p.T);
   int chunks = 0;
   for (int g0 = kWave; g0 < d; g0 += kWave) {
     const int j = g0 + lane;
     uint32_t lo = 0, hi = 0;
     int c = 0;
     if (j < d) {
-      const uint32_t b = static_cast<uint32_t>(p.c_col[pb + j]) * static_cast<uint32_t>(p.T) +
-                         static_cast<uint32_t>(S.t);
-      lo = p.tile_off[b];
-      hi = p.tile_off[b + 1];
+      const uint32_t b = static_cast<uint32_t>(p.c_col[pb + j]) * T + static_cast<uint32_t>(S.t);
+      lo = off[b];
+      hi = off[b + 1];
       c = p.c_val[pb + j];
     }
     Stage E = S;
@@ -454,8 +605,8 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
     chunks += E.G.nq;
     for (int b = 0; b < E.nb; ++b) {
       Batch B;
-      issue1(E, b, p.tile_ent, lane, B);
-      scatter_any<true>(B, E, acc, 0u, kLabMask1, kS1);
+      issue1(E, b, ent, lane, B);
+      scatter_f<F>(B, E, acc, u8h);
     }
   }
   return chunks;
@@ -466,7 +617,7 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
 #ifndef DPS_W5_KPL
 #define DPS_W5_KPL 1
 #endif
-template <int KPL, bool HV>
+template <int F, int KPL, bool HV>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DPS_W5_KPL ? 5 : 4))) void k_cct1(CctParams p) {
   // LDS: the accumulator at address 0 (scatter ORs the in-tile offset into 0)
   // then the candidate queue.
@@ -517,7 +668,48 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
         v = p.c_col[pb + lane];
         vT = static_cast<uint32_t>(v) * static_cast<uint32_t>(p.T);
       }
-      if (d0 > 1) sort_venues<HV>(p, d0, lane, c, vT, v);
+      if (d0 > 1) sort_venues<HV || F == 2>(p, d0, lane, c, vT, v);
+      // dual (F = 2): wide tiles run as two u8 halves of the companion set
+      const bool dual = F == 2 && p.h_ent != nullptr;
+      const uint32_t vT8 = dual ? static_cast<uint32_t>(v) * static_cast<uint32_t>(p.T8) : 0u;
+      Win1 w;
+      int h_next = -1;            // the second half of a split wide tile, pending
+      uint32_t h_ub = 0;
+      // bound of u8 half t8 over the row's venues (wave sum of C[x,v] * maxc;
+      // rows with more than 64 venues, or a product beyond 16 bits, keep ub4)
+      auto half_ub = [&](int t8, uint32_t ub4) -> uint32_t {
+        if (!p.use_bounds || d > kWave) return ub4;
+        const uint32_t mx = lane < d0 ? p.h_maxc[vT8 + static_cast<uint32_t>(t8)] : 0u;
+        const uint32_t pr = static_cast<uint32_t>(c) * mx;
+        if (ballot(mx > 0xFFFFu || pr > 0xFFFFu)) return ub4;
+        return wave_sum_u32(pr);
+      };
+      // next stage: the pending half, else the next live tile -- split into its
+      // two u8 halves when dual and its 4-bit bound exceeds 15
+      auto choose = [&](double tau, int& tn, uint32_t& ubn, bool& u8n) {
+        u8n = false;
+        if (h_next >= 0) {
+          tn = h_next;
+          ubn = h_ub;
+          u8n = true;
+          h_next = -1;
+          return;
+        }
+        tn = next_tile(p, w, t_end, pb, d, c, vT, lane, tau, gxf, ubn);
+        if (!dual || tn < 0 || ubn <= Fmt<F>::UB0) return;
+        const int ta = 2 * tn, tb = 2 * tn + 1;
+        const uint32_t ua = half_ub(ta, ubn);
+        const uint32_t ubb = tb < p.T8 ? half_ub(tb, ubn) : 0u;
+        u8n = true;
+        if (ua == 0) {            // only the second half holds this row's entries
+          tn = tb;
+          ubn = ubb;
+          return;
+        }
+        tn = ta;
+        ubn = ua;
+        if (ubb > 0) { h_next = tb; h_ub = ubb; }
+      };
       // venue skipping: lane j < d0 holds venue j's heavy-table slot (-1: none)
       // and an upper bound of C[x,v] / s_v (s_v >= C[x,v] > 0)
       uint32_t hv = 0;          // hv_pack(C[x,v] / s_v rounded up, slot)
@@ -528,35 +720,39 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
           hv = hv_pack(static_cast<float>(static_cast<double>(c) / static_cast<double>(p.s[v])) *
                            (1.0f + 0x1p-20f), sl);
       }
-      Win1 w;
       win_load(p, w, t_beg, t_beg, t_end, pb, d, c, vT, lane, -1.0, gxf);
       uint32_t ub_t = 0;
-      const int t0 = next_tile(p, w, t_end, pb, d, c, vT, lane, -1.0, gxf, ub_t);
+      int t0;
+      bool u8n;
+      choose(-1.0, t0, ub_t, u8n);
       if (t0 >= 0) {
         Pend1 P;
-        pend_load(p, P, t0, ub_t, d0, vT, lane);
+        pend_load<F, HV>(p, P, t0, ub_t, u8n, d0, vT, vT8, lane);
         Stage1 X;
-        stage_make(X, P, c, d0, 0ull, lane);
+        stage_make<F>(X, P, c, d0, 0ull, lane);
         bool hchg = false;        // H grew at the last stage boundary
         Batch B;
-        issue1(X.S, 0, p.tile_ent, lane, B);
-        const int t1 = next_tile(p, w, t_end, pb, d, c, vT, lane, -1.0, gxf, ub_t);
-        pend_load(p, P, t1, ub_t, d0, vT, lane);
+        issue1(X.S, 0, X.u8h ? p.h_ent : p.tile_ent, lane, B);
+        int t1;
+        choose(-1.0, t1, ub_t, u8n);
+        pend_load<F, HV>(p, P, t1, ub_t, u8n, d0, vT, vT8, lane);
         for (;;) {
           const int npass = 1 << X.S.lnp;
           bool more = false;
           for (X.S.pass = 0; X.S.pass < npass; ++X.S.pass) {
             if (prof) ts[0] = __builtin_amdgcn_s_memtime();
-            if (X.S.pass > 0) issue1(X.S, 0, p.tile_ent, lane, B);
-            scatter_any<true>(B, X.S, acc, 0u, kLabMask1, kS1);
+            const uint32_t* ent = X.u8h ? p.h_ent : p.tile_ent;
+            if (X.S.pass > 0) issue1(X.S, 0, ent, lane, B);
+            scatter_f<F>(B, X.S, acc, X.u8h);
             for (int b = 1; b < X.S.nb; ++b) {
               Batch B2;
-              issue1(X.S, b, p.tile_ent, lane, B2);
-              scatter_any<true>(B2, X.S, acc, 0u, kLabMask1, kS1);
+              issue1(X.S, b, ent, lane, B2);
+              scatter_f<F>(B2, X.S, acc, X.u8h);
             }
             n_chunk += static_cast<uint64_t>(X.S.G.nq);
             ++n_pass;
-            if (d > kWave) n_chunk += static_cast<uint64_t>(extra_groups(p, X.S, acc, pb, d, lane));
+            if (d > kWave)
+              n_chunk += static_cast<uint64_t>(extra_groups<F>(p, X.S, acc, pb, d, lane, X.u8h));
             if (prof) ts[1] = __builtin_amdgcn_s_memtime();
             // score what is queued while the list is filling or the queue is
             // half full (one memory round trip per 64 candidates)
@@ -566,15 +762,20 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
             int mseg = 1;
             if (tau > 0.0) {
               if (HV && hm) {
-                // M_Q >= tau (gx + gs) / 2 - rho gs, rounded down (fp32, every
-                // rounding to nearest; the factors keep it below the exact value)
+                // two lower bounds of the M_Q a target needs, the larger wins:
+                //  M_Q >= tau (gx + gs) / 2 - rho gs   (M_H <= rho g[y]; rounded
+                //    down in fp32, every rounding to nearest, the factors keep it
+                //    below the exact value), and
+                //  M_Q >= mneed(tau, gx + gs) - ubh     (M_H <= ubh, integers)
                 float rho = 0.0f;   // >= max_{h in H} C[x,h] / s_h
                 for (uint64_t m = hm; m; m &= m - 1)
                   rho = fmaxf(rho, hv_ratio(readlane(hv, __builtin_ctzll(m))));
                 const float gs = X.gsf;
                 const float r = static_cast<float>(tau) * (gxf + gs) * (0.5f * (1.0f - 0x1p-19f)) -
                                 rho * gs * (1.0f + 0x1p-17f);
-                mseg = r >= 2147483000.0f ? INT32_MAX : r > 1.0f ? static_cast<int>(ceilf(r)) : 1;
+                const int m1 = r >= 2147483000.0f ? INT32_MAX : r > 1.0f ? static_cast<int>(ceilf(r)) : 1;
+                const int m2 = mneed_lo32(static_cast<float>(tau), gxf + gs) - X.ubh;
+                mseg = m1 > m2 ? m1 : m2;
               } else {
                 const int mn = mneed_lo32(static_cast<float>(tau), gxf + X.gsf);
                 mseg = mn > 1 ? mn : 1;
@@ -582,6 +783,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
             }
             const bool last = X.S.pass + 1 == npass;
             Stage S = X.S;
+            const bool u8S = F == 1 || X.u8h;   // this stage's counters: u8 format
             const uint64_t hmS = hm;   // this stage's H (the update below is for the next)
             if (prof) ts[2] = __builtin_amdgcn_s_memtime();
             if (last) {
@@ -604,20 +806,27 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
                 }
               }
               more = P.t >= 0 && !row_done;
-              if (more) stage_make(X, P, c, d0, hm, lane);
+              if (more) stage_make<F>(X, P, c, d0, hm, lane);
               else X.S.G.nq = 0;
               if (prof) ts[5] = __builtin_amdgcn_s_memtime();
-              issue1(X.S, 0, p.tile_ent, lane, B);
+              issue1(X.S, 0, X.u8h ? p.h_ent : p.tile_ent, lane, B);
               if (prof) ts[6] = __builtin_amdgcn_s_memtime();
-              const int tn = more ? next_tile(p, w, t_end, pb, d, c, vT, lane, tau, gxf, ub_t) : -1;
-              pend_load(p, P, tn, ub_t, d0, vT, lane);
+              int tn = -1;
+              if (more) choose(tau, tn, ub_t, u8n);
+              pend_load<F, HV>(p, P, tn, ub_t, u8n, d0, vT, vT8, lane);
             }
             if (prof) ts[3] = __builtin_amdgcn_s_memtime();
             if (S.lnp == 0) {
-              epi1_u8<KPL, HV>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
-                               hmS, n_ver);
+              if (u8S)
+                epi1_u8<KPL, HV>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
+                                 hmS, n_ver);
+              else
+                epi1_u4<KPL, HV>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
+                                 hmS, n_ver);
+            } else if (u8S) {
+              epi1_wide<1, KPL, HV>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, n_ver);
             } else {
-              epi1_wide<KPL, HV>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, n_ver);
+              epi1_wide<F, KPL, HV>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, n_ver);
             }
             // the queue holds counts that miss hmS: complete them before the
             // next stage's (larger) H applies
@@ -686,7 +895,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
   }
 }
 
-template <int KPL>
+template <int F, int KPL>
 int launch1(const CctParams& p, hipStream_t st) {
   int dev = 0, n_cu = 256;
   DPS_HIP_RET(hipGetDevice(&dev));
@@ -698,21 +907,29 @@ int launch1(const CctParams& p, hipStream_t st) {
 #endif
   int64_t grid = static_cast<int64_t>(n_cu) * wpc;
   if (grid > p.n_rows) grid = p.n_rows;
-  if (p.hv_c) k_cct1<KPL, true><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
-  else k_cct1<KPL, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  if (p.hv_c) k_cct1<F, KPL, true><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  else k_cct1<F, KPL, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
   DPS_LAUNCHED();
   return DPS_OK;
 }
 
 }  // namespace
 
-// Lean kernel for W = 8192 (shift 13), one wave per row; the caller has
-// validated the parameters and zeroed p.counter.
+// Lean kernel for W = 8192 (shift 13, u8 counters) and W = 16384 (shift 14,
+// 4-bit counters), one wave per row; the caller has validated the parameters
+// and zeroed p.counter.
 int cct1_launch(const CctParams& p, hipStream_t st) {
-  if (p.shift != kS1) return DPS_ERR_INVALID;
-  if (p.k <= 64) return launch1<1>(p, st);
-  if (p.k <= 128) return launch1<2>(p, st);
-  return launch1<4>(p, st);
+  if (p.shift == 13) {
+    if (p.k <= 64) return launch1<1, 1>(p, st);
+    if (p.k <= 128) return launch1<1, 2>(p, st);
+    return launch1<1, 4>(p, st);
+  }
+  if (p.shift == 14) {
+    if (p.k <= 64) return launch1<2, 1>(p, st);
+    if (p.k <= 128) return launch1<2, 2>(p, st);
+    return launch1<2, 4>(p, st);
+  }
+  return DPS_ERR_INVALID;
 }
 
 }  // namespace dps

@@ -53,6 +53,13 @@ struct CctParams {
   const int32_t* hv_slot;
   const uint16_t* hv_c;
   int n_hv;
+  // W = 16384 (4-bit counters) only: the same C^T cut at 8192 with u8-counter
+  // entries (null = off): a tile whose 4-bit bound exceeds 15 runs as its two
+  // u8 halves instead of wide 4-bit passes
+  const uint32_t* h_off;
+  const uint32_t* h_ent;
+  const uint32_t* h_maxc;
+  int64_t T8;
 };
 
 // Lean one-wave kernel for W = 8192 (dps_cct1.hip).

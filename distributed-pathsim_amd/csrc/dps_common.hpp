@@ -142,11 +142,14 @@ __device__ __forceinline__ int wave_bitonic_sort(int v) {
 // ---- several dword ranges set in one launch (dps_scan.hip) ---------------------
 // Replaces a hipMemsetAsync per small array (each one a fill kernel of its own).
 struct FillSet {
-  uint32_t* p[8];
-  int64_t n[8];    // dwords
-  uint32_t v[8];
+  static constexpr int kMax = 8;
+  uint32_t* p[kMax];
+  int64_t n[kMax];    // dwords
+  uint32_t v[kMax];
   int k = 0;
+  bool overflow = false;   // an add() beyond kMax ranges (fill_set refuses to run)
   void add(void* ptr, int64_t n_words, uint32_t value) {
+    if (k >= kMax) { overflow = true; return; }
     p[k] = static_cast<uint32_t*>(ptr);
     n[k] = n_words;
     v[k] = value;

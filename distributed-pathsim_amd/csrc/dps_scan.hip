@@ -139,6 +139,7 @@ __global__ __launch_bounds__(256) void k_fill_set(FillSet s) {
 }  // namespace
 
 hipError_t fill_set(const FillSet& s, hipStream_t stream) {
+  if (s.overflow) return hipErrorInvalidValue;   // more ranges than FillSet::kMax
   if (s.k == 0) return hipSuccess;
   int64_t longest = 1;
   for (int r = 0; r < s.k; ++r) longest = s.n[r] > longest ? s.n[r] : longest;

@@ -10,8 +10,10 @@
 //                      into power-of-two pieces (e <= 7; e <= 5 when l % 4 == 3,
 //                      since e = 6, 7 with l % 4 == 3 are the padding codes) --
 //                      the kernel's adds are linear in C, so the pieces sum
-//                      exactly; wider tiles -> packed uint32 (C[y,v] << 16) |
-//                      (label - t*W);
+//                      exactly; W = 16384 -> packed uint16 (l << 2) | e, the
+//                      same scheme for packed 4-bit counters (e <= 3; e <= 1
+//                      when l % 8 == 7, whose e = 2, 3 are the padding codes);
+//                      wider tiles -> packed uint32 (C[y,v] << 16) | (label - t*W);
 //   dps_walk_row / dps_row_scores / dps_pair_count: one source row, as the
 //                      reference's run() loop computes it (:30-52).
 #include "dps_common.hpp"
@@ -43,18 +45,31 @@ __device__ __forceinline__ int64_t label_of(const int32_t* rank, int64_t y) {
 
 constexpr int64_t kTileGminLds = 4096;   // tiles whose g minimum is reduced in LDS
 
-// Entry format (see the file header): 16-bit entries for shift <= 13.
-// A 16-bit entry (l << 3) | e adds C[x,v] * 2^e to target l: in the hot
-// kernel's packed-u8 accumulators that is C[x,v] << (8*(l % 4) + e) -- the
-// entry's low five bits ARE the shift.  Codes e = 6, 7 at l % 4 == 3 are
-// reserved for padding (real pieces there stop at 2^5): a bucket's padding is
-// groups of {2^7, 2^7} or {2^7, 2^6, 2^6} on one dword, each adding
-// C[x,v] * 2^32 == 0 to it, so padding needs no multiply by a zero count.
-constexpr int kP16MaxShift = 13;
-__device__ __forceinline__ uint32_t p16_max_e(uint32_t lab) { return (lab & 3u) == 3u ? 5u : 7u; }
-__device__ __forceinline__ uint32_t n_pieces(bool p16, uint32_t c, uint32_t lab) {
-  if (!p16) return 1u;
-  const uint32_t me = p16_max_e(lab);
+// Entry formats (see the file header), by tile width:
+//  kFmtU8  (shift <= 13): uint16 (l << 3) | e adds C[x,v] * 2^e to target l: in
+//          the hot kernel's packed-u8 accumulators that is C[x,v] << (8*(l % 4)
+//          + e) -- the entry's low five bits ARE the shift.  Codes e = 6, 7 at
+//          l % 4 == 3 are reserved for padding (real pieces there stop at 2^5):
+//          a bucket's padding is groups of {2^7, 2^7} or {2^7, 2^6, 2^6} on one
+//          dword, each adding C[x,v] * 2^32 == 0 to it, so padding needs no
+//          multiply by a zero count.
+//  kFmtU4  (shift == 14): uint16 (l << 2) | e, the same for packed 4-bit
+//          counters: C[x,v] << (4*(l % 8) + e) is again the low five bits; codes
+//          e = 2, 3 at l % 8 == 7 are the padding groups {2^3, 2^3} / {2^3, 2^2,
+//          2^2} (shift 31, 31 / 31, 30, 30), real pieces there stop at 2^1.
+//  kFmt32  (shift >= 15): uint32 (C[y,v] << 16) | l.
+constexpr int kFmt32 = 0, kFmtU8 = 1, kFmtU4 = 2;
+__host__ __device__ __forceinline__ int tile_fmt(int shift) {
+  return shift <= 13 ? kFmtU8 : shift == 14 ? kFmtU4 : kFmt32;
+}
+__device__ __forceinline__ uint32_t ent_lsh(int fmt) { return fmt == kFmtU8 ? 3u : 2u; }
+__device__ __forceinline__ uint32_t ent_max_e(int fmt, uint32_t lab) {
+  if (fmt == kFmtU8) return (lab & 3u) == 3u ? 5u : 7u;
+  return (lab & 7u) == 7u ? 1u : 3u;
+}
+__device__ __forceinline__ uint32_t n_pieces(int fmt, uint32_t c, uint32_t lab) {
+  if (fmt == kFmt32) return 1u;
+  const uint32_t me = ent_max_e(fmt, lab);
   return (c >> me) + static_cast<uint32_t>(__popc(c & ((1u << me) - 1u)));
 }
 // Bucket size in entries after padding to 16 B (4 uint32 / 8 uint16 entries).
@@ -66,17 +81,17 @@ __device__ __forceinline__ uint32_t padded_count(uint32_t tot, uint32_t per16) {
   return r;
 }
 // Write the entries of (c, local label) at entry index i (16- or 32-bit units).
-__device__ __forceinline__ void put_entry(bool p16, uint32_t* ent, int64_t i, uint32_t c,
+__device__ __forceinline__ void put_entry(int fmt, uint32_t* ent, int64_t i, uint32_t c,
                                           uint32_t lab) {
-  if (!p16) {
+  if (fmt == kFmt32) {
     ent[i] = (c << 16) | lab;
     return;
   }
   uint16_t* e16 = reinterpret_cast<uint16_t*>(ent);
-  const uint32_t me = p16_max_e(lab);
-  for (uint32_t n = c >> me; n > 0; --n) e16[i++] = static_cast<uint16_t>((lab << 3) | me);
+  const uint32_t me = ent_max_e(fmt, lab), sh = ent_lsh(fmt);
+  for (uint32_t n = c >> me; n > 0; --n) e16[i++] = static_cast<uint16_t>((lab << sh) | me);
   for (uint32_t r = c & ((1u << me) - 1u); r != 0; r &= r - 1u)
-    e16[i++] = static_cast<uint16_t>((lab << 3) | static_cast<uint32_t>(__ffs(r) - 1));
+    e16[i++] = static_cast<uint16_t>((lab << sh) | static_cast<uint32_t>(__ffs(r) - 1));
 }
 
 __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict__ c_ptr,
@@ -109,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
       const int32_t c = c_val[j];
       if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
       const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
-      atomicAdd(&cnt[b], n_pieces(shift <= kP16MaxShift, static_cast<uint32_t>(c),
+      atomicAdd(&cnt[b], n_pieces(tile_fmt(shift), static_cast<uint32_t>(c),
                                   static_cast<uint32_t>(label_of(rank, y))));
       // C = 1 (most entries when buckets are sparse) needs no atomic: k_round4
       // raises the maximum of every non-empty bucket to at least 1
@@ -136,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, i
 
 __global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__ off, int P,
                                                      const uint32_t* __restrict__ cursor,
-                                                     int64_t n, uint32_t lab_mask, bool p16,
+                                                     int64_t n, uint32_t lab_mask, int fmt,
                                                      uint32_t* __restrict__ ent) {
   // Bucket b spans off[b*P] .. off[(b+1)*P) (P parts per bucket), its first
   // cursor[b] entries are real.  Padding entries have C = 0 (they add nothing)
@@ -148,16 +163,21 @@ __global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__
     const int64_t np = off[(b + 1) * P] - i0;
     for (int64_t k = 0; k < np; ++k) {
       const int64_t i = i0 + k;
-      if (!p16) {
-        ent[i] = (static_cast<uint32_t>(i) << 2) & lab_mask;
+      if (fmt == kFmt32) {
+        ent[i] = (static_cast<uint32_t>(i) << 2) & lab_mask & ~3u;
         continue;
       }
-      // groups on one dword: {7, 6, 6} first when the count is odd, then {7, 7}
+      // groups on one dword: {hi, lo, lo} first when the count is odd, then
+      // {hi, hi}; hi / lo = 7 / 6 (u8 counters, label % 4 == 3) or 3 / 2
+      // (4-bit counters, label % 8 == 7)
       const bool odd = (np & 1) != 0;
       const int64_t grp = odd ? (k < 3 ? 0 : 1 + (k - 3) / 2) : k / 2;
-      const uint32_t e = (odd && (k == 1 || k == 2)) ? 6u : 7u;
-      const uint32_t lab = ((static_cast<uint32_t>(i0 + 2 * grp) << 2) & lab_mask) | 3u;
-      reinterpret_cast<uint16_t*>(ent)[i] = static_cast<uint16_t>((lab << 3) | e);
+      const bool u8 = fmt == kFmtU8;
+      const uint32_t hi = u8 ? 7u : 3u;
+      const uint32_t e = (odd && (k == 1 || k == 2)) ? hi - 1u : hi;
+      const uint32_t lab = u8 ? (((static_cast<uint32_t>(i0 + 2 * grp) << 2) & lab_mask & ~3u) | 3u)
+                              : (((static_cast<uint32_t>(i0 + 2 * grp) << 3) & lab_mask & ~7u) | 7u);
+      reinterpret_cast<uint16_t*>(ent)[i] = static_cast<uint16_t>((lab << ent_lsh(fmt)) | e);
     }
   }
 }
@@ -189,10 +209,10 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restri
     for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
       const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
       const uint32_t c = static_cast<uint32_t>(c_val[j]);
-      const bool p16 = shift <= kP16MaxShift;
+      const int fmt = tile_fmt(shift);
       const uint32_t l = static_cast<uint32_t>(lab) & ymask;
-      const uint32_t pos = atomicAdd(&cursor[b], n_pieces(p16, c, l));
-      put_entry(p16, ent, off[b] + pos, c, l);
+      const uint32_t pos = atomicAdd(&cursor[b], n_pieces(fmt, c, l));
+      put_entry(fmt, ent, off[b] + pos, c, l);
     }
   }
 }
@@ -483,7 +503,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
   if (static_cast<int>(sb) >= sr.n_sub) return;   // block-uniform: before any barrier
   for (int v = threadIdx.x; v < mr.n; v += kBlkThreads) { cnt_s[v] = 0; mx_s[v] = 0; }
   if (threadIdx.x == 0) { gmin_s = ~0ull; ovf_s = 0; }
-  const bool p16 = shift <= kP16MaxShift;
+  const int fmt = tile_fmt(shift);
   const int64_t l0 = part * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
   const int64_t t = l0 >> shift;
@@ -500,7 +520,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
     if (c > 0xFFFF) ovf_s = 1;
     const uint32_t lv = static_cast<uint32_t>(v - mr.m0);
     if (lv >= static_cast<uint32_t>(mr.n)) return;   // another block's mid range
-    atomicAdd(&cnt_s[lv], n_pieces(p16, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
+    atomicAdd(&cnt_s[lv], n_pieces(fmt, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
     if (c > 1) atomicMax(&mx_s[lv], static_cast<uint32_t>(c));   // 1 by k_tile_parts_fix
   });
   __syncthreads();
@@ -565,7 +585,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
   const SubRange sr = sub_range(part_n[part], sb, S);
   if (static_cast<int>(sb) >= sr.n_sub) return;   // block-uniform: before any barrier
   for (int v = threadIdx.x; v < mr.n; v += kBlkThreads) cnt_s[v] = 0;
-  const bool p16 = shift <= kP16MaxShift;
+  const int fmt = tile_fmt(shift);
   const int64_t l0 = part * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
   const int64_t t = l0 >> shift;
@@ -584,7 +604,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
     walk_strips(R, nl, sr.e0, sr.e1, tab_s, c_col, c_val, [&](int i, int32_t v, int32_t c) {
       const uint32_t lv = static_cast<uint32_t>(v - mr.m0);
       if (lv >= static_cast<uint32_t>(mr.n)) return;
-      atomicAdd(&cnt_s[lv], n_pieces(p16, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
+      atomicAdd(&cnt_s[lv], n_pieces(fmt, static_cast<uint32_t>(c), lab0 + static_cast<uint32_t>(i)));
     });
     __syncthreads();
     for (int lv = threadIdx.x; lv < mr.n; lv += kBlkThreads) {
@@ -601,8 +621,8 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
     const uint32_t lab = lab0 + static_cast<uint32_t>(i);
     const unsigned long long pos =
         atomicAdd(&base_s[lv], static_cast<unsigned long long>(
-                                  n_pieces(p16, static_cast<uint32_t>(c), lab)));
-    put_entry(p16, ent, static_cast<int64_t>(pos), static_cast<uint32_t>(c), lab);
+                                  n_pieces(fmt, static_cast<uint32_t>(c), lab)));
+    put_entry(fmt, ent, static_cast<int64_t>(pos), static_cast<uint32_t>(c), lab);
   });
 }
 
@@ -628,12 +648,14 @@ __global__ __launch_bounds__(kBlock) void k_walk_row(const int32_t* __restrict__
       const int cx = src_val[j];
       for (uint32_t i = off[b] + threadIdx.x; i < off[b + 1]; i += kBlock) {
         const uint32_t w = ent[i];
-        if (shift <= kP16MaxShift) {   // two 16-bit entries per word (W = P here)
+        const int fmt = tile_fmt(shift);
+        if (fmt != kFmt32) {   // two 16-bit entries per word (W = P here)
+          const uint32_t sh = ent_lsh(fmt);
 #pragma unroll
           for (int half = 0; half < 2; ++half) {
             const uint32_t h = (w >> (16 * half)) & 0xFFFFu;
-            const uint32_t e = h & 7u, lab = h >> 3;
-            if ((lab & 3u) == 3u && e >= 6u) continue;   // padding
+            const uint32_t e = h & ((1u << sh) - 1u), lab = h >> sh;
+            if (e > ent_max_e(fmt, lab)) continue;   // padding
             atomicAdd(&acc[lab], cx << e);
           }
           continue;
@@ -777,7 +799,7 @@ int64_t dps_ct_tiles_ent_capacity(int64_t nnz, int64_t sum_c, int64_t n_mids,
   if (tile_w <= 0 || nnz < 0 || sum_c < nnz) return 0;
   const int64_t T = (n_targets + tile_w - 1) / tile_w;
   const int64_t nb = n_mids * (T > 0 ? T : 1);
-  if (log2_exact(tile_w) > kP16MaxShift) return nnz + 3 * (nb < nnz ? nb : nnz) + 4;
+  if (tile_fmt(log2_exact(tile_w)) == kFmt32) return nnz + 3 * (nb < nnz ? nb : nnz) + 4;
   // 16-bit entries: power-of-two pieces, at most (c + 1) / 2 <= 1 + (c - 1) / 2
   // per C entry; up to 9 padding entries per non-empty bucket; two entries per
   // uint32 word
@@ -842,7 +864,8 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   const int64_t nblk = (n_targets + lpb - 1) / lpb;
   const int S = tile_sub();
   DPS_REQUIRE(nblk * S * n_ranges < INT32_MAX, DPS_ERR_OVERFLOW, "too many tile-build blocks");
-  const bool p16 = shift <= kP16MaxShift;   // counts and offsets are in entries
+  const int fmt = tile_fmt(shift);
+  const bool p16 = fmt != kFmt32;   // 16-bit entries: counts and offsets are in entries
   const uint32_t per16 = p16 ? 8u : 4u;
   const bool fused_parts = blk && n_targets > 0 && nblk <= kPartLds;
   if (blk) {   // every counter, the status word and the tile minima in one launch
@@ -900,7 +923,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     }
     if (nb > 0) {
       k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(
-          off64, P, cnt, nb, ((static_cast<uint32_t>(tile_w) - 1u) & ~3u), p16, tile_ent);
+          off64, P, cnt, nb, static_cast<uint32_t>(tile_w) - 1u, fmt, tile_ent);
       DPS_LAUNCHED();
     }
     return DPS_OK;
@@ -929,7 +952,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   }
   if (nb > 0) {
     k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(
-        off64, 1, cursor, nb, ((static_cast<uint32_t>(tile_w) - 1u) & ~3u), p16, tile_ent);
+        off64, 1, cursor, nb, static_cast<uint32_t>(tile_w) - 1u, fmt, tile_ent);
     DPS_LAUNCHED();
   }
   return DPS_OK;

@@ -28,10 +28,12 @@ STATS_LEN = 8
 TUNE_WAVES_PER_ROW, TUNE_TILE_BUILD = 1, 2
 
 
-class VenueSkip(C.Structure):
-    """struct dps_venue_skip (include/dpathsim.h): device pointers + n_hv."""
+class CctExt(C.Structure):
+    """struct dps_cct_ext (include/dpathsim.h): venue skipping (s, hv_slot,
+    hv_c, n_hv) and the companion u8 tiles of tile_w 16384 (half_*)."""
     _fields_ = [("s", C.c_void_p), ("hv_slot", C.c_void_p), ("hv_c", C.c_void_p),
-                ("n_hv", C.c_int32)]
+                ("n_hv", C.c_int32), ("half_off", C.c_void_p), ("half_ent", C.c_void_p),
+                ("half_maxc", C.c_void_p)]
 
 _i32 = C.c_int32
 _i64 = C.c_int64

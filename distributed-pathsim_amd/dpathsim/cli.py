@@ -134,7 +134,9 @@ def main(argv=None):
         eng.topk(k, r0, r1, out=tuple(o[: r1 - r0] for o in out))
         torch.cuda.synchronize(dev)
         compute_s = time.perf_counter() - t0
-        den = eng.tensor("den")[:na].cpu().numpy()
+        # the log's "global walk" lines print the global walk g (the reference's
+        # metapath_global_walk, DPathSim_APVPA.py:30,46) whatever the denominator
+        walks = eng.tensor("g")[:na].cpu().numpy()
         pairs = max(na - 1, 0) * (r1 - r0)
         per_pair = compute_s / max(pairs, 1)
         t1 = time.perf_counter()
@@ -146,7 +148,7 @@ def main(argv=None):
                 tuple(o[: r1 - r0] for o in out)
             if rank == 0:
                 idx, cnt, sc = (t.cpu().numpy() for t in res)
-                write_topk_log(out_path, typed, idx, cnt, sc, den, append=True,
+                write_topk_log(out_path, typed, idx, cnt, sc, walks, append=True,
                                stage_seconds=per_pair,
                                overall_seconds=time.perf_counter() - t0)
                 metrics["log"] = out_path

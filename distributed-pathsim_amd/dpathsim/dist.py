@@ -285,11 +285,21 @@ def read_topk_shards(directory):
         raise FileNotFoundError(f"no topk shards in {directory}")
     metas.sort(key=lambda m: m["row_begin"])
     world = metas[0]["world"]
-    if len(metas) != world:
+    if len(metas) != world or any(m["world"] != world for m in metas):
         raise ValueError(f"{len(metas)} shard files for world {world}")
+    if metas[0]["row_begin"] != 0:
+        raise ValueError("the first shard does not start at row 0")
+    k = metas[0]["k"]
+    if any(m["k"] != k for m in metas):
+        raise ValueError("shards disagree on k")
     for a, b in zip(metas, metas[1:]):
         if a["row_end"] != b["row_begin"]:
             raise ValueError("shards do not tile the rows")
-    blocks = [np.load(os.path.join(directory, f"topk_rank{m['rank']:05d}.npy"), allow_pickle=False)
-              for m in metas]
+    blocks = []
+    for m in metas:
+        arr = np.load(os.path.join(directory, f"topk_rank{m['rank']:05d}.npy"), allow_pickle=False)
+        if arr.shape != (m["row_end"] - m["row_begin"], 2 * k) or arr.dtype != np.int64:
+            raise ValueError(f"shard of rank {m['rank']} has shape {arr.shape} {arr.dtype}, "
+                             f"manifest says {m['row_end'] - m['row_begin']} x {2 * k} int64")
+        blocks.append(arr)
     return unpack_topk(torch.from_numpy(np.concatenate(blocks)))

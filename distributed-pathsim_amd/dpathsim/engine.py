@@ -18,7 +18,9 @@ import torch
 from . import _lib
 from .graph import TypedTables
 
-DEFAULT_TILE_W = 8192
+# one tile of 16384 targets per wave: 4-bit counters in 8 KiB of LDS (tiles
+# whose bound exceeds 15 take wider passes); 8192 = u8 counters
+DEFAULT_TILE_W = 16384
 DEFAULT_SPLIT_ROWS = 256    # heaviest rows of a launch cut into pieces
 DEFAULT_PIECES = 16         # target-tile ranges per split row
 DEFAULT_HEAVY_VENUES = 32   # venue skipping: heavy venues in the dense table (64-byte rows)
@@ -92,7 +94,9 @@ class PathSimEngine:
         # venue skipping (dps_venue_skip): exact, row-sum denominator only
         self.venue_skip = DEFAULT_VENUE_SKIP and denominator == "rowsum"
         self.n_heavy = DEFAULT_HEAVY_VENUES
-        self._vskip = None
+        # tile_w 16384: the companion 8192-target u8 tiles for wide tiles
+        self.half_tiles = True
+        self._ext = None
         # load balance of the hot kernel: the split_rows heaviest rows of a
         # launch are cut into `pieces` target-tile ranges (see topk())
         self.split_rows = DEFAULT_SPLIT_ROWS
@@ -273,6 +277,23 @@ class PathSimEngine:
                       _ptr(tile_maxc), _ptr(tile_gmin), _ptr(status), _ptr(tws), tws.numel(), st)
             mark("tiles")
             del tws
+            half = None
+            if self.tile_w == 16384 and self.half_tiles:
+                # companion u8 tiles at 8192: a tile whose 4-bit bound exceeds 15
+                # runs as its two halves from these (dps_cct_ext)
+                T8 = max(1, math.ceil(NA / 8192)) if NA else 1
+                h_off = self._empty(NV * T8 + 1, torch.int32)
+                h_maxc = self._empty(NV * T8 + 1, torch.int32)
+                h_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV, NA, 8192)
+                h_ent = self._empty(h_cap, torch.int32)
+                h_status = self._empty(1, torch.int32)
+                hws = self._ws(_lib.size("dps_ct_tiles_workspace_size", NV, NA, 8192))
+                _lib.call("dps_ct_tiles_build", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), None,
+                          _ptr(t_rank), NA, NV, 8192, _ptr(h_off), _ptr(h_ent), _ptr(h_maxc), None,
+                          _ptr(h_status), _ptr(hws), hws.numel(), st)
+                del hws
+                half = (h_off, h_ent, h_maxc, h_status)
+                mark("half_tiles")
             hv_slot = hv_c = None
             if self.venue_skip and self.denominator == "rowsum" and NA and NV:
                 # venue skipping: the heavy venues (most author entries) and the
@@ -290,10 +311,16 @@ class PathSimEngine:
                  t_perm=t_perm, t_rank=t_rank, tile_off=tile_off, tile_ent=tile_ent,
                  tile_maxc=tile_maxc, tile_gmin=tile_gmin, stats=stats, status=status,
                  ap_nnz=ap_nnz, px_nnz=px_nnz, sp_status=sp_status, hv_slot=hv_slot, hv_c=hv_c,
+                 half_off=half[0] if half else None, half_ent=half[1] if half else None,
+                 half_maxc=half[2] if half else None, half_status=half[3] if half else None,
                  topk_ws=self._ws(_lib.size("dps_cct_topk_workspace_size")))
-        self._vskip = None
-        if hv_c is not None:
-            self._vskip = _lib.VenueSkip(_ptr(s), _ptr(hv_slot), _ptr(hv_c), min(self.n_heavy, 64))
+        self._ext = None
+        if hv_c is not None or half is not None:
+            self._ext = _lib.CctExt(
+                _ptr(s) if hv_c is not None else None, _ptr(hv_slot), _ptr(hv_c),
+                min(self.n_heavy, 64) if hv_c is not None else 0,
+                _ptr(half[0]) if half else None, _ptr(half[1]) if half else None,
+                _ptr(half[2]) if half else None)
         self.built = True
         if timed:
             torch.cuda.synchronize(self.device)
@@ -310,8 +337,9 @@ class PathSimEngine:
             raise RuntimeError("call build() first")
         d = self._dev
         info = self.info
+        status = d["status"] if d.get("half_status") is None else d["status"] | d["half_status"]
         host = torch.cat([d["stats"], d["ap_nnz"], d["px_nnz"], d["c_nnz"][:1],
-                          d["status"].to(torch.int64), d["sp_status"].to(torch.int64)]).cpu()
+                          status.to(torch.int64), d["sp_status"].to(torch.int64)]).cpu()
         # nnz over the author rows (C also holds the untyped author_of rows)
         L = _lib.STATS_LEN
         info.max_c = int(host[_lib.STAT_MAX_C])
@@ -349,11 +377,11 @@ class PathSimEngine:
         return {"dequeued": int(w[0]), "passes": int(w[1]), "chunks": int(w[2]),
                 "verified": int(w[3])}
 
-    def _vskip_arg(self):
-        """Host pointer to the dps_venue_skip struct (None = off)."""
-        if self._vskip is None or not self.venue_skip:
+    def _ext_arg(self):
+        """Host pointer to the dps_cct_ext struct (None = no extension)."""
+        if self._ext is None:
             return None
-        return C.addressof(self._vskip)
+        return C.addressof(self._ext)
 
     @property
     def n_targets(self):
@@ -409,7 +437,7 @@ class PathSimEngine:
                   _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA, self.typed.n_mids,
                   self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
                   _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]),
-                  self._vskip_arg())
+                  self._ext_arg())
         with torch.cuda.device(self.device):
             dq = None
             if heavy_first and R > 1:
@@ -467,7 +495,7 @@ class PathSimEngine:
                       _ptr(d["den"]), _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA,
                       self.typed.n_mids, self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
                       _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]),
-                      self._vskip_arg(), _ptr(order), R, int(k), _ptr(tmp[0]), _ptr(tmp[1]), _ptr(tmp[2]),
+                      self._ext_arg(), _ptr(order), R, int(k), _ptr(tmp[0]), _ptr(tmp[1]), _ptr(tmp[2]),
                       _ptr(d["topk_ws"]), d["topk_ws"].numel(), self.stream)
             for o, t in zip(out, tmp):
                 o[perm] = t

@@ -282,7 +282,16 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
                        void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
- * Venue skipping for the hot kernel (an exact pruning; no reference
+ * Hot-kernel extensions, passed as one host struct (dps_cct_ext, nullable):
+ *
+ * (1) Companion u8 tiles for tile_w = 16384.  The 16384-target tiles carry
+ *   16-bit entries for packed 4-bit counters (dps_ct_tiles_build); a tile
+ *   whose per-row bound exceeds 15 needs wider counters.  With half_off /
+ *   half_ent / half_maxc = dps_ct_tiles_build of the SAME C and t_rank at
+ *   tile_w 8192, such a tile runs as its two 8192-target halves from those u8
+ *   tiles; without them it takes wide 4-bit passes (slower, same results).
+ *
+ * (2) Venue skipping (an exact pruning; no reference
  * counterpart -- the reference counts every path of the motif,
  * DPathSim_APVPA.py:90-109).  With the row-sum denominator every target has
  * g[y] = sum_v C[y,v] s[v] (metapath_global_walk :70-88), so once a
@@ -300,17 +309,22 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
  *   label(y) * n_hv + hv_slot[v] = C[y,v] for every author row y < n_targets
  *   and heavy venue v, 0 elsewhere; label(y) = t_rank[y] (NULL = y).  Needs
  *   max C <= 65535 (the engine's check).
- * dps_venue_skip: what the top-k entry points take (host struct, nullable =
- *   off).  Valid ONLY when their g is the row-sum global walk g = C.s for this
- *   s (not with the diag denominator); hv_c must use the same t_rank.  Used by
- *   the W = 8192 kernel; other tile widths ignore it.
+ * Venue skipping is valid ONLY when the top-k call's g is the row-sum global
+ *   walk g = C.s for this s (not with the diag denominator); hv_c must use the
+ *   same t_rank.  Used by the one-wave kernel (tile_w 8192 and 16384); other
+ *   tile widths ignore it.
  * ------------------------------------------------------------------------- */
-typedef struct dps_venue_skip {
+typedef struct dps_cct_ext {
+  /* (2) venue skipping; s == NULL: off */
   const int64_t* s;          /* s[v] = column sums of C over every AP row (dps_walks_fused) */
   const int32_t* hv_slot;    /* [n_mids], dps_heavy_venues */
   const uint16_t* hv_c;      /* [n_targets * n_hv], dps_heavy_table */
   int32_t n_hv;              /* 1..64 */
-} dps_venue_skip;
+  /* (1) companion u8 tiles (tile_w 16384 only); half_ent == NULL: off */
+  const uint32_t* half_off;
+  const uint32_t* half_ent;
+  const uint32_t* half_maxc;
+} dps_cct_ext;
 int dps_heavy_venues(const uint32_t* n_v, int64_t n_mids, int32_t n_hv, int32_t* hv_slot,
                      void* stream);
 int dps_heavy_table(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
@@ -328,7 +342,7 @@ int dps_heavy_table(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c
  * dps_target_order (all NULL = identity labels, g_t = g); tile_* from
  * dps_ct_tiles_build with the same t_rank (tile_gmin required, tile_maxc
  * optional -- enables skipping tiles that cannot hold a top-k candidate);
- * vskip: venue skipping (above), NULL = off.
+ * ext: companion u8 tiles / venue skipping (above), NULL = neither.
  * Outputs (row-major [row_end-row_begin][k], output row x - row_begin):
  * out_idx int32 (original ordinals), out_cnt int64 (M), out_score double.
  * 1 <= k <= 256.  row_order (nullable, int32[row_end-row_begin]): a
@@ -342,7 +356,7 @@ int dps_cct_topk(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
                  const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
                  const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                  const uint32_t* tile_off, const uint32_t* tile_ent,
-                 const uint32_t* tile_maxc, const int64_t* tile_gmin, const dps_venue_skip* vskip,
+                 const uint32_t* tile_maxc, const int64_t* tile_gmin, const dps_cct_ext* ext,
                  int64_t row_begin, int64_t row_end, const int32_t* row_order, int32_t k,
                  int32_t* out_idx, int64_t* out_cnt, double* out_score,
                  void* ws, size_t ws_bytes, void* stream);
@@ -356,7 +370,7 @@ int dps_cct_topk_rows(const int64_t* c_ptr, const int32_t* c_col, const int32_t*
                       const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                       const uint32_t* tile_off, const uint32_t* tile_ent,
                       const uint32_t* tile_maxc, const int64_t* tile_gmin,
-                      const dps_venue_skip* vskip, const int32_t* rows,
+                      const dps_cct_ext* ext, const int32_t* rows,
                       int64_t n_rows, int32_t k, int32_t* out_idx, int64_t* out_cnt,
                       double* out_score, void* ws, size_t ws_bytes, void* stream);
 
@@ -382,7 +396,7 @@ int dps_cct_topk_split(const int64_t* c_ptr, const int32_t* c_col, const int32_t
                        const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
                        const uint32_t* tile_off, const uint32_t* tile_ent,
                        const uint32_t* tile_maxc, const int64_t* tile_gmin,
-                       const dps_venue_skip* vskip, int64_t row_begin,
+                       const dps_cct_ext* ext, int64_t row_begin,
                        int64_t row_end, const int32_t* row_order, int64_t n_order,
                        const int32_t* piece_t0, const int32_t* piece_t1, int64_t n_pieces,
                        int32_t* piece_idx, int64_t* piece_cnt, double* piece_score, int32_t k,

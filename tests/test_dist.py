@@ -263,3 +263,31 @@ def test_rccl_capi_compact_gather_one_rank(tmp_path):
     mp.start_processes(_rccl_capi_worker, args=(1, _free_port(), 10, str(out)), nprocs=1,
                        join=True, start_method="spawn")
     assert out.read_text() == "ok"
+
+
+def test_read_topk_shards_rejects_stale_or_mixed(tmp_path):
+    """A shard directory whose manifests do not start at row 0, disagree on k,
+    or whose arrays do not match their manifest is refused, not merged."""
+    import json
+    from dpathsim.dist import write_topk_shard
+    k = 3
+    parts = [tuple(torch.zeros((n, k), dtype=dt) for dt in (torch.int32, torch.int64, torch.float64))
+             for n in (4, 6)]
+    bounds = [(0, 4), (4, 10)]
+    for r in range(2):
+        write_topk_shard(str(tmp_path), r, 2, bounds, parts[r], k)
+    assert read_topk_shards(str(tmp_path))[0].shape == (10, k)
+    m1 = tmp_path / "topk_rank00001.json"
+    meta = json.loads(m1.read_text())
+    m1.write_text(json.dumps(dict(meta, k=4)))
+    with pytest.raises(ValueError, match="k"):
+        read_topk_shards(str(tmp_path))
+    m1.write_text(json.dumps(meta))
+    np.save(tmp_path / "topk_rank00001.npy", np.zeros((5, 2 * k), np.int64))
+    with pytest.raises(ValueError, match="shape"):
+        read_topk_shards(str(tmp_path))
+    m0 = tmp_path / "topk_rank00000.json"
+    meta0 = json.loads(m0.read_text())
+    m0.write_text(json.dumps(dict(meta0, row_begin=1)))
+    with pytest.raises(ValueError, match="row 0"):
+        read_topk_shards(str(tmp_path))

@@ -13,27 +13,36 @@ def _counts(eng):
     return int(w[1]), int(w[2])
 
 
-def test_lean_counters_without_tile_skipping():
-    """With tile skipping off every tile of every row is scanned with four
-    32-bit passes: passes = 4 T * rows(d > 0), chunks = 4 * sum_x sum_{v in x}
-    (entries of v over all tiles) / 4 words."""
-    from dpathsim.engine import build_engine
+@pytest.mark.parametrize("tile_w,half,npass", [(8192, False, 4), (16384, False, 8),
+                                               (16384, True, 4)])
+def test_lean_counters_without_tile_skipping(tile_w, half, npass):
+    """With tile skipping off every tile of every row is scanned with 32-bit
+    counters: 4 passes of 2048 targets per 8192-target tile (W = 8192, and W =
+    16384 whose unbounded tiles run as two u8 halves of the companion tiles),
+    8 per 4-bit W = 16384 tile without companions.  So passes = npass * T * rows
+    (d > 0), chunks = npass * sum_x sum_{v in x} (words of v over all tiles) / 4,
+    T and the words those of the tile set the passes read."""
+    from dpathsim.engine import PathSimEngine
     from dpathsim.synth import synth_dblp
-    t = synth_dblp(20_000, 60_000, 500, seed=7).typed()
-    eng = build_engine(t, tile_w=8192)
+    t = synth_dblp(40_000, 120_000, 500, seed=7).typed()
+    eng = PathSimEngine(t, tile_w=tile_w)
+    eng.half_tiles = half
+    eng.upload().build()
     na, nv = t.n_authors, t.n_mids
-    T = (na + 8191) // 8192
+    tw = 8192 if half else tile_w
+    T = (na + tw - 1) // tw
     cp = eng.tensor("c_ptr")[: na + 1].cpu().numpy()
     cc = eng.tensor("c_col")[: cp[-1]].cpu().numpy().astype(np.int64)
-    off = eng.tensor("tile_off")[: nv * T + 1].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    off = eng.tensor("half_off" if half else "tile_off")[: nv * T + 1].cpu().numpy().astype(np.int64)
+    off &= 0xFFFFFFFF
     words_v = off[(np.arange(nv) + 1) * T] - off[np.arange(nv) * T]
     assert (words_v % 4 == 0).all()
     rows_nonempty = int((np.diff(cp) > 0).sum())
     eng.tile_skip = False
     eng.topk(10, 0, na, heavy_first=False)
     n_pass, n_chunk = _counts(eng)
-    assert n_pass == 4 * T * rows_nonempty
-    assert n_chunk == 4 * int((words_v[cc] // 4).sum())
+    assert n_pass == npass * T * rows_nonempty
+    assert n_chunk == npass * int((words_v[cc] // 4).sum())
     # with tile skipping: fewer, and the same again on a re-run (counts are per launch)
     eng.tile_skip = True
     eng.topk(10, 0, na)

@@ -197,6 +197,26 @@ def test_spgemm_long_and_huge_rows(multi, spgemm):
     _same([a.cpu().numpy() for a in eng.topk(10)], co.topk(10, 0, na))
 
 
+@pytest.mark.parametrize("tile_w", [8192, 16384])
+@pytest.mark.parametrize("k", [10, 100])
+def test_split_rows_identical_lean(tile_w, k):
+    """The lean one-wave kernel's split path (the production shape): pieces of
+    the heaviest rows over several target tiles, k > 64 (two top-k registers),
+    row sub-ranges -- bit for bit the unsplit rows."""
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_dblp
+    t = synth_dblp(40_000, 120_000, 400, seed=17).typed()
+    eng = build_engine(t, tile_w=tile_w)
+    assert -(-t.n_authors // tile_w) >= 3
+    whole = [a.cpu().numpy() for a in eng.topk(k, split_rows=0)]
+    for r0, r1 in ((0, t.n_authors), (1000, 21000)):
+        for M, P in ((256, 16), (100, 3)):
+            got = [a.cpu().numpy() for a in eng.topk(k, r0, r1, split_rows=M, pieces=P)]
+            for a, b in zip(got, whole):
+                assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
+                                      (b.view(np.int64) if b.dtype == np.float64 else b)[r0:r1])
+
+
 @pytest.mark.parametrize("M,P,k", [(40, 4, 10), (300, 16, 10), (64, 7, 100), (5, 64, 3)])
 def test_split_rows_identical(M, P, k):
     """Heavy rows cut into target-tile pieces (dps_cct_topk_split + the merge)

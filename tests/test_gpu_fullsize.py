@@ -1,13 +1,16 @@
-"""Full-size parity: the HIP path against the C oracle at BASELINE.json's sizes.
+"""Full-size parity: the HIP path against the C oracle at BASELINE.json's sizes,
+every launch through eng.topk -- the bench's entry point (heaviest rows first,
+the 256 heaviest split into target-tile pieces, dps_topk_merge):
 
-* config3 (1M authors, the bench workload, tile_w 8192 = 16-bit entries, one
-  wave per row): EVERY row, bit-exact (idx, count, score bits);
-* config4 (APTPA, 200k topics): the 5000 heaviest rows by row work plus every
-  row with more than 64 topics (the general, non-register path);
-* config5 (3M authors, 20k venues, top-100): the 2000 heaviest rows plus every
-  row whose per-tile bound sum_v C[x,v] * maxc[v,t] exceeds 255 in some tile
-  (the rows that can take the u16 / u32 accumulator passes);
-* a crafted graph whose counts force the u16 and u32 passes at tile_w 8192;
+* config3 (1M authors, the bench workload, tile_w 16384 = 4-bit counters, one
+  wave per row): EVERY row, bit-exact (idx, count, score bits); and the u8
+  format (tile_w 8192) identical to it on every row;
+* config4 (APTPA, 200k topics, top-10): EVERY row;
+* config5 (3M authors, 20k venues, top-100, two top-k registers per lane):
+  every third row plus the 2000 heaviest rows plus every row whose per-tile
+  bound sum_v C[x,v] * maxc[v,t] exceeds 255 in some tile (the rows that can
+  take the wide accumulator passes);
+* a crafted graph whose counts force the wide passes at tile_w 8192 and 16384;
 * config 2 stand-in (dblp_large.gexf is absent, .MISSING_LARGE_BLOBS:1;
   SURVEY §8d): config3_100k written as GEXF, re-read by the streaming loader
   (timed), built, and compared row for row.
@@ -56,31 +59,37 @@ def _topk_rows(eng, k, rows):
 
 def test_config3_all_rows_bench_shape():
     import pathsim_oracle as po
-    from dpathsim.engine import build_engine
+    from dpathsim.engine import DEFAULT_TILE_W, build_engine
     from dpathsim.synth import synth_config
     t = synth_config("config3").typed()
-    eng = build_engine(t, tile_w=8192)              # the bench configuration
-    got = eng.topk(10)
+    eng = build_engine(t)                           # the bench configuration
+    assert eng.tile_w == DEFAULT_TILE_W == 16384
+    got = [a.cpu().numpy() for a in eng.topk(10)]
     t0 = time.perf_counter()
     co = po.COracle.from_typed(t)
     want = _oracle_rows(co, 10, np.arange(t.n_authors), chunk=100_000)
     print(f"oracle: all {t.n_authors} rows in {time.perf_counter() - t0:.1f} s")
     _cmp(got, want)
+    del eng
+    u8 = build_engine(t, tile_w=8192)               # the u8-counter format
+    _cmp(u8.topk(10), want)
 
 
-def test_config4_heaviest_and_wide_rows():
+def test_config4_all_rows():
     import pathsim_oracle as po
     from dpathsim.engine import build_engine
     from dpathsim.graph import APTPA
     from dpathsim.synth import synth_config
     t = synth_config("config4").typed(APTPA)
     eng = build_engine(t)
-    work = eng.row_work().cpu().numpy()
     d = np.diff(eng.tensor("c_ptr")[: t.n_authors + 1].cpu().numpy())
-    rows = np.union1d(np.argsort(-work, kind="stable")[:5000], np.flatnonzero(d > 64))
-    assert (d > 64).sum() > 0
-    print(f"config4: {len(rows)} rows ({(d > 64).sum()} with > 64 topics)")
-    _cmp(_topk_rows(eng, 10, rows), _oracle_rows(po.COracle.from_typed(t), 10, rows), rows)
+    assert (d > 64).sum() > 0                       # rows of the extra-group path
+    got = [a.cpu().numpy() for a in eng.topk(10)]   # heavy-first + split + merge
+    t0 = time.perf_counter()
+    want = _oracle_rows(po.COracle.from_typed(t), 10, np.arange(t.n_authors), chunk=100_000)
+    print(f"config4: oracle on all {t.n_authors} rows ({(d > 64).sum()} with > 64 topics) "
+          f"in {time.perf_counter() - t0:.1f} s")
+    _cmp(got, want)
 
 
 def _wide_bound_rows(eng, t, cap=3000):
@@ -107,7 +116,7 @@ def _wide_bound_rows(eng, t, cap=3000):
     return np.asarray(out, dtype=np.int64)
 
 
-def test_config5_heaviest_and_wide_bound_rows():
+def test_config5_strided_heaviest_and_wide_bound_rows():
     import pathsim_oracle as po
     from dpathsim.engine import build_engine
     from dpathsim.synth import synth_config
@@ -116,9 +125,14 @@ def test_config5_heaviest_and_wide_bound_rows():
     work = eng.row_work().cpu().numpy()
     wide = _wide_bound_rows(eng, t)
     assert len(wide) > 0
-    rows = np.union1d(np.argsort(-work, kind="stable")[:2000], wide)
-    print(f"config5: {len(rows)} rows ({len(wide)} with a tile bound > 255)")
-    _cmp(_topk_rows(eng, 100, rows), _oracle_rows(po.COracle.from_typed(t), 100, rows), rows)
+    rows = np.union1d(np.union1d(np.argsort(-work, kind="stable")[:2000], wide),
+                      np.arange(0, t.n_authors, 3))
+    got = [a.cpu().numpy()[rows] for a in eng.topk(100)]   # bench path, k = 100
+    t0 = time.perf_counter()
+    want = _oracle_rows(po.COracle.from_typed(t), 100, rows, chunk=50_000)
+    print(f"config5: {len(rows)} rows ({len(wide)} with a tile bound > 255), oracle "
+          f"{time.perf_counter() - t0:.1f} s")
+    _cmp(got, want, rows)
 
 
 def _crafted_wide_counts(n_fill=20000, seed=5):
@@ -157,12 +171,13 @@ def _crafted_wide_counts(n_fill=20000, seed=5):
                  ["author_of", "submit_at"], node_ids=lambda i: f"n{i}", labels=lambda i: f"L{i}")
 
 
+@pytest.mark.parametrize("tile_w", [8192, 16384])
 @pytest.mark.parametrize("k", [10, 100])
-def test_crafted_u16_u32_passes_at_8192(k):
+def test_crafted_wide_passes(k, tile_w):
     import pathsim_oracle as po
     from dpathsim.engine import build_engine
     t = _crafted_wide_counts().typed()
-    eng = build_engine(t, tile_w=8192)
+    eng = build_engine(t, tile_w=tile_w)
     assert eng.info.max_diag > 65535                # M[x,x] beyond u16: the u32 pass runs
     co = po.COracle.from_typed(t)
     _cmp(eng.topk(k), co.topk(k, 0, t.n_authors))

@@ -29,20 +29,21 @@ def _same(got, want, r0=0):
                            f"want {oi[bad[0]]} {oc[bad[0]]} {os_[bad[0]]}")
 
 
-def _pair(t, **kw):
+def _pair(t, tile_w=8192, **kw):
     from dpathsim.engine import build_engine
-    on = build_engine(t, tile_w=8192, venue_skip=True, **kw)
-    off = build_engine(t, tile_w=8192, venue_skip=False, **kw)
-    assert on._vskip is not None and off._vskip is None
+    on = build_engine(t, tile_w=tile_w, venue_skip=True, **kw)
+    off = build_engine(t, tile_w=tile_w, venue_skip=False, **kw)
+    assert on._ext is not None and on._ext.s and (off._ext is None or not off._ext.s)
     return on, off
 
 
+@pytest.mark.parametrize("tile_w", [8192, 16384])
 @pytest.mark.parametrize("k", [10, 100])
-def test_venue_skip_synth_exact_and_fires(k):
+def test_venue_skip_synth_exact_and_fires(k, tile_w):
     import pathsim_oracle as po
     from dpathsim.synth import synth_dblp
     t = synth_dblp(60_000, 180_000, 800, seed=13).typed()
-    on, off = _pair(t)
+    on, off = _pair(t, tile_w)
     got = _np(on.topk(k, heavy_first=False))
     cnt = on.kernel_counts()
     ref = _np(off.topk(k, heavy_first=False))
@@ -55,13 +56,14 @@ def test_venue_skip_synth_exact_and_fires(k):
     assert cnt["chunks"] < cnt_off["chunks"]
 
 
-def test_venue_skip_split_pieces_and_wide_rows():
+@pytest.mark.parametrize("tile_w", [8192, 16384])
+def test_venue_skip_split_pieces_and_wide_rows(tile_w):
     """The bench entry point (heavy-first, split pieces + merge) on a graph with
     rows of > 64 venues and heavily shared venues (large counts)."""
     import pathsim_oracle as po
     from dpathsim.synth import synth_dblp
     t = synth_dblp(40_000, 200_000, 3_000, seed=21, mid_alpha=1.1, authors_lambda=3.0).typed()
-    on, off = _pair(t)
+    on, off = _pair(t, tile_w)
     d = np.diff(on.tensor("c_ptr")[: t.n_authors + 1].cpu().numpy())
     assert d.max() > 64
     got = _np(on.topk(10, split_rows=64, pieces=4))
@@ -89,4 +91,4 @@ def test_venue_skip_diag_denominator_is_off():
     from dpathsim.synth import synth_dblp
     t = synth_dblp(5_000, 15_000, 200, seed=2).typed()
     eng = build_engine(t, tile_w=8192, denominator="diag")
-    assert eng._vskip is None and eng.tensor("hv_c") is None
+    assert (eng._ext is None or not eng._ext.s) and eng.tensor("hv_c") is None

@@ -32,7 +32,8 @@ k = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 nrows = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 W = int(os.environ.get("SIM_W", "8192"))
 SEG = 1024
-KH = int(os.environ.get("SIM_KH", "0"))     # H restricted to the KH venues of largest n_v (0: any)
+KH = int(os.environ.get("SIM_KH", "0"))
+TIGHT = int(os.environ.get("SIM_TIGHT", "0"))   # also bound M_H by sum_{h in H} a_h maxc[h,t]     # H restricted to the KH venues of largest n_v (0: any)
 t0 = time.time()
 g = synth_config(cfg)
 t = g.typed()
@@ -81,7 +82,7 @@ def better_insert(best_s, best_y, sc, yy):
 
 
 res = {"old_tiles": 0, "old_chunks": 0, "tiles": 0, "chunks": 0, "verify": 0, "qfrac": 0.0,
-       "hv_tiles": 0, "mism": 0, "nib": 0, "u8": 0}
+       "hv_tiles": 0, "mism": 0, "nib": 0, "u8": 0, "old_cand": 0, "cand": 0}
 tb0 = time.time()
 for i0 in range(0, nrows, 25):
     rr = rows[i0:i0 + 25]
@@ -129,6 +130,13 @@ for i0 in range(0, nrows, 25):
             res["old_chunks"] += ch[:, tt].sum()
             e = slice(st[tt], st[tt + 1])
             yy = np.unique(ys[e])
+            if tau > 0:
+                gs = gseg[rank[yy] // SEG]
+                ok = Mfull[yy] >= np.ceil(tau * (gx + gs) * 0.5 * EPS - 1e-9)
+                res["old_cand"] += int(ok.sum())
+                yy = yy[ok]
+            else:
+                res["old_cand"] += len(yy)
             scy = 2.0 * Mfull[yy] / (gx + gg[yy])
             best_s, best_y = better_insert(best_s, best_y, scy, yy)
         # --- venue skipping
@@ -160,9 +168,17 @@ for i0 in range(0, nrows, 25):
             MQ = np.bincount(yq, weights=a[js[e][qe]] * bs[e][qe])
             yy = np.unique(yq)
             mq = MQ[yy]
+            if tau <= 0:
+                res["cand"] += len(yy)
             if tau > 0:
                 gs = gseg[rank[yy] // SEG]
-                cand = mq >= np.ceil(tau * gx / 2 * EPS + coef * gs * EPS - 1e-9)
+                thr = tau * gx / 2 * EPS + coef * gs * EPS
+                if TIGHT and (~q).any():
+                    # M_H(y) <= sum_{h in H} a_h maxc[h, t] as well
+                    ubh = float((a[~q] * maxc[vx[~q], tt]).sum())
+                    thr = np.maximum(thr, np.ceil(tau * (gx + gs) * 0.5 * EPS) - ubh)
+                cand = mq >= np.ceil(thr - 1e-9)
+                res["cand"] += int(cand.sum())
                 if (~q).any():
                     res["hv_tiles"] += 1
                     res["verify"] += int(cand.sum())
