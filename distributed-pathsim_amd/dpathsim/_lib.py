@@ -12,6 +12,8 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPATHSIM_LIB", os.path.join(_HERE, "libdpathsim.so"))
 
+ABI_VERSION = 2  # DPS_ABI_VERSION in include/dpathsim.h
+
 DPS_OK = 0
 DPS_ERR_INVALID = -1
 DPS_ERR_HIP = -2
@@ -148,6 +150,10 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.dps_abi_version() != ABI_VERSION:
+            raise DPSLibraryError(
+                f"{LIB_PATH} has ABI {lib.dps_abi_version()}, the bindings expect {ABI_VERSION}: "
+                "rebuild it")
         _lib = lib
         return lib
 
