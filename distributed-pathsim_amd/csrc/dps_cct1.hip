@@ -81,6 +81,42 @@ template <> struct Fmt<2> {
 #endif
 constexpr int kEpi1 = DPS_EPI1;                // epilogue blocks read per trip
 
+// Zero the kEpi1 KiB of accumulator an epilogue trip has just read (dwords b0..).
+// DPS_ZERO_ADDTID: ds_write_addtid_b32 (address = M0 + offset + 4 * lane, no
+// address VGPR: 128 B/clk/CU against ~79 for ds_write_b128, MI355X_MICROARCH.md
+// §LDS); M0 is saved and restored inside the statement.  The wave's LDS
+// operations run in order, so the reads issued before it see the old values.
+#ifndef DPS_ZERO_ADDTID
+#define DPS_ZERO_ADDTID 0
+#endif
+__device__ __forceinline__ void zero_trip(uint32_t* acc, int b0, int lane) {
+#if DPS_ZERO_ADDTID
+  static_assert(kEpi1 == 2, "offsets below cover two 1 KiB blocks");
+  uint32_t save;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "ds_write_addtid_b32 %2 offset:0\n\t"
+      "ds_write_addtid_b32 %2 offset:256\n\t"
+      "ds_write_addtid_b32 %2 offset:512\n\t"
+      "ds_write_addtid_b32 %2 offset:768\n\t"
+      "ds_write_addtid_b32 %2 offset:1024\n\t"
+      "ds_write_addtid_b32 %2 offset:1280\n\t"
+      "ds_write_addtid_b32 %2 offset:1536\n\t"
+      "ds_write_addtid_b32 %2 offset:1792\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(save)
+      : "s"(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(b0 * 4))), "v"(0u)
+      : "memory");
+  (void)acc;
+  (void)lane;
+#else
+#pragma unroll
+  for (int i = 0; i < kEpi1; ++i)
+    *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
+#endif
+}
+
 // 64 consecutive tiles of one row: lane l describes tile w0 + l.
 struct Win1 {
   int w0;          // first tile of the window (wave-uniform)
@@ -417,9 +453,7 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
 #pragma unroll
     for (int i = 0; i < kEpi1; ++i)
       a[i] = *reinterpret_cast<const uint4*>(acc + b0 + i * kWave * 4 + lane * 4);
-#pragma unroll
-    for (int i = 0; i < kEpi1; ++i)
-      *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
+    zero_trip(acc, b0, lane);
 #pragma unroll
     for (int i = 0; i < kEpi1; ++i) block(a[i], (b0 >> 8) + i);
   }
@@ -520,9 +554,7 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
 #pragma unroll
     for (int i = 0; i < kEpi1; ++i)
       a[i] = *reinterpret_cast<const uint4*>(acc + b0 + i * kWave * 4 + lane * 4);
-#pragma unroll
-    for (int i = 0; i < kEpi1; ++i)
-      *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
+    zero_trip(acc, b0, lane);
 #pragma unroll
     for (int i = 0; i < kEpi1; ++i) block(a[i], (b0 >> 8) + i);
   }

@@ -31,7 +31,9 @@ for W, NW in cases:
             e0.record(); o = eng.topk(K, 0, R); e1.record(); torch.cuda.synchronize()
             best = min(best, e0.elapsed_time(e1))
         o = [a.cpu().numpy() for a in o]
-        print(f"{cfg} W={W} NW={NW}: {best:.1f} ms for {R} rows (k={K})", flush=True)
+        import hashlib
+        dig = hashlib.sha1(b"".join(a.tobytes() for a in o)).hexdigest()[:16]
+        print(f"{cfg} W={W} NW={NW}: {best:.2f} ms for {R} rows (k={K}) digest {dig}", flush=True)
         if ref is None:
             ref = o
         else:

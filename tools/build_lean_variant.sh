@@ -8,5 +8,5 @@ mkdir -p ../../ab
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -I. -Wall -Wno-unused-function \
   -Wno-pass-failed -munsafe-fp-atomics "$@" -c dps_cct1.hip -o /tmp/cct1_$name.o
 objs=$(ls build/*.o | grep -v dps_cct1)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../ab/libdpathsim_$name.so /tmp/cct1_$name.o $objs
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../ab/libdpathsim_$name.so /tmp/cct1_$name.o $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo built ab/libdpathsim_$name.so

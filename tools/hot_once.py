@@ -7,7 +7,7 @@ from dpathsim.engine import build_engine
 
 R = int(os.environ.get("HOT_ROWS", "100000"))
 eng = build_engine(synth_config(os.environ.get("HOT_CONFIG", "config3")).typed(),
-                   tile_w=int(os.environ.get("HOT_W", "8192")))
+                   tile_w=int(os.environ.get("HOT_W", "16384")))
 torch.cuda.synchronize()
 eng.topk(10, 0, R)
 torch.cuda.synchronize()

@@ -7,7 +7,7 @@ import torch
 from dpathsim.synth import synth_config
 from dpathsim.engine import build_engine
 
-eng = build_engine(synth_config(os.environ.get("AB_CONFIG", "config3")).typed(), tile_w=8192)
+eng = build_engine(synth_config(os.environ.get("AB_CONFIG", "config3")).typed(), tile_w=int(os.environ.get("AB_W", "16384")))
 R = eng.typed.n_authors
 for ab in ("0", "16"):
     os.environ["DPATHSIM_ABLATE"] = ab

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counters of the hot kernel at HEAD on the bench launch (config3, all 1M
-# rows, tile_w 8192, k 10), one rocprofv3 --pmc pass per counter group
+# rows, tile_w $HOT_W (default 16384), k 10), one rocprofv3 --pmc pass per counter group
 # (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE in separate passes; <= 8 SQ
 # counters per pass), then tools/pmc_hot_summary.py -> gpurun_out/pmc_hot.json.
 set -u
@@ -8,6 +8,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 export HOT_ROWS=${HOT_ROWS:-1000000}
+export HOT_W=${HOT_W:-16384}
 declare -A PASS
 PASS[fetch]="FETCH_SIZE"
 PASS[write]="WRITE_SIZE"

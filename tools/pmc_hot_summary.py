@@ -40,7 +40,8 @@ for p in ("fetch", "write", "valu", "lds"):
     if os.path.isdir(d):
         vals, n = read(d)
         c.update({f"{k}@{p}" if k == "GRBM_GUI_ACTIVE" else k: v for k, v in vals.items()})
-rec = {"kernel": "k_cct1 (dps_cct_topk, W = 8192)", "config": "config3", "world": 1, "tile_w": 8192, "k": 10,
+W = int(os.environ.get("HOT_W", "16384"))
+rec = {"kernel": f"k_cct1 (dps_cct_topk, W = {W})", "config": "config3", "world": 1, "tile_w": W, "k": 10,
        "rows": int(os.environ.get("HOT_ROWS", "1000000")), "counters_per_launch": c}
 if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
     rec["hbm_bytes_per_launch"] = 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
