@@ -170,19 +170,21 @@ def main():
     value = pairs / (elapsed / args.steps)
 
     # ---- roofline of the dominant kernel (dps_cct_topk -> k_cct1), measured live --
-    # The kernel is bound by latency at the occupancy LDS capacity allows (5 waves
-    # per SIMD, 8 KB of accumulator each); of the resources it uses the LDS array
-    # is the busiest (PMC), so the roofline is LDS, priced per instruction class
-    # (DESIGN.md §9): per launch the kernel counts its accumulator passes and the
-    # 16-byte chunks it scatters (workspace words 1, 2);
-    #   scatter  32 B per chunk of ds_add_u32 (b32 store class, 64 B/clk/CU),
-    #   read     8 KiB per pass of ds_read_b128 (256 B/clk/CU),
-    #   zero     8 KiB per pass of ds_write_b128 (79 B/clk/CU),
+    # ALGORITHMIC work of one launch (the SIMT path's unit is one
+    # term C[x,v]*C[y,v], sum_{x in shard} sum_{v in x} n_v of them), priced on the
+    # LDS per instruction class (MI355X_MICROARCH.md §LDS):
+    #   scatter  one ds_add_u32 per term, 4 B (b32 store class, 64 B/clk/CU);
+    #   read     the packed counters of every (row, target) pair once, 1/2 B per
+    #            pair at 4-bit counters (tile_w 16384), 1 B at u8 (ds_read_b128,
+    #            256 B/clk/CU);
+    #   zero     the same bytes rewritten (ds_write_b128, 79 B/clk/CU);
     # floor = sum of bytes / rate / (256 CUs x 2.4 GHz); frac = floor / launch time
     # (events on the kernel's stream).  `achieved` / `peak` express the same in
-    # b128-read-equivalent bytes (each class scaled by 256 / its rate).
-    # HBM (secondary, logical): 16 B per chunk scattered + 64 B per candidate
-    # completed from the heavy-venue table + 20 B per output slot + row offsets.
+    # b128-read-equivalent bytes.  This work is fixed by the problem: venue and
+    # tile skipping do less of it (the executed counts -- passes, chunks -- are
+    # reported beside it, with their own floor), which shows as a higher frac.
+    # HBM (secondary, logical): 2 B per term (16-bit C^T entries) + 20 B per
+    # output slot + row offsets; `traffic` = PMC bytes of the same launch.
     topk_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_topk]))
     r0, r1 = bounds0[rank]
     shard = r1 - r0
@@ -193,30 +195,39 @@ def main():
     w = torch.zeros(nnz + 1, dtype=torch.int64, device=dev)
     w[1:] = torch.cumsum(n_v[c_col], 0)
     terms = int((w[c_ptr[r1]] - w[c_ptr[r0]]).item())      # sum_{x in shard} sum_{v in x} n_v
-    ent_bytes = 2 if args.tile_w <= 8192 else 4
+    ent_bytes = 2 if args.tile_w <= 16384 else 4
     kc = eng.kernel_counts()                         # the last launch's counts
     n_pass, n_chunk, n_ver = kc["passes"], kc["chunks"], kc["verified"]
-    if n_chunk:
-        bytes_launch = 16 * n_chunk + 64 * n_ver + 20 * shard * k + 8 * (shard + 1)
-    else:   # kernels other than k_cct1 count nothing: every entry of the row's venues
-        bytes_launch = ent_bytes * terms + 20 * shard * k + 8 * (shard + 1)
+    bytes_launch = ent_bytes * terms + 20 * shard * k + 8 * (shard + 1)
     hbm_achieved = bytes_launch / (topk_ms * 1e-3) / 1e9
-    lds_cls = {"scatter_add_b32": 32 * n_chunk, "acc_read_b128": 8192 * n_pass,
-               "acc_zero_b128": 8192 * n_pass}
+    ctr_bytes = 0.5 if args.tile_w == 16384 else 1.0 if args.tile_w <= 8192 else 4.0
+    pairs_launch = shard * (NA - 1)
     lds_rate = {"scatter_add_b32": LDS_ADD_B32, "acc_read_b128": LDS_READ_B128,
                 "acc_zero_b128": LDS_WRITE_B128}
-    lds_floor_ms = {c: b / lds_rate[c] / (N_CU * CLK_GHZ * 1e9) * 1e3 for c, b in lds_cls.items()}
+
+    def lds_price(cls):
+        floor = {c: b / lds_rate[c] / (N_CU * CLK_GHZ * 1e9) * 1e3 for c, b in cls.items()}
+        equiv = sum(b * LDS_READ_B128 / lds_rate[c] for c, b in cls.items())
+        return floor, equiv
+
+    lds_cls = {"scatter_add_b32": 4 * terms, "acc_read_b128": int(ctr_bytes * pairs_launch),
+               "acc_zero_b128": int(ctr_bytes * pairs_launch)}
+    lds_floor_ms, lds_equiv = lds_price(lds_cls)
     lds_bytes = sum(lds_cls.values())
-    lds_equiv = sum(b * LDS_READ_B128 / lds_rate[c] for c, b in lds_cls.items())
-    # only the lean W = 8192 kernel (k_cct1) counts its passes and chunks
-    lds_achieved = lds_equiv / (topk_ms * 1e-3) / 1e9 if n_pass > 0 else None
+    lds_achieved = lds_equiv / (topk_ms * 1e-3) / 1e9
+    # executed: what the kernel counted (k_cct1 only: 16-byte chunks scattered, 8 KiB
+    # accumulator passes read and zeroed)
+    exe_cls = {"scatter_add_b32": 32 * n_chunk, "acc_read_b128": 8192 * n_pass,
+               "acc_zero_b128": 8192 * n_pass}
+    exe_floor_ms, _ = lds_price(exe_cls)
     traffic, pmc = None, {}
     if args.pmc_json and os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
             if (pm.get("config") == args.config and pm.get("world", 1) == world
                     and pm.get("tile_w", args.tile_w) == args.tile_w and args.scale == 1.0
-                    and pm.get("k", k) == k and args.denominator == "rowsum"):
+                    and pm.get("k", k) == k and args.denominator == "rowsum"
+                    and pm.get("venue_skip", False) == bool(eng._ext is not None and eng._ext.s)):
                 traffic = pm.get("hbm_bytes_per_launch")
                 pmc = {key: pm.get(key) for key in ("lds", "valu", "wait")}
         except Exception:
@@ -311,18 +322,22 @@ def main():
                        "n_authors": NA, "k": k, "tile_w": args.tile_w,
                        "nnz_C": info.nnz_c, "sum_terms": terms if world == 1 else None,
                        "parallelism": f"row-shard x{world} (work-balanced, heaviest rows first)"},
-            # bound: the busiest resource per the HEAD counters (LDS array; the
-            # kernel is latency-bound at the occupancy its LDS allows)
+            # bound: the LDS array (the resource the algorithm's unit work lands on;
+            # the kernel itself is issue/latency-bound at the occupancy its LDS
+            # allows)
             "roofline": {"bound": "lds", "kernel": f"dps_cct_topk (k_cct1, W {args.tile_w})",
                          "achieved": lds_achieved, "peak": LDS_PEAK_GBS,
                          "unit": "GB/s (ds_read_b128-equivalent)",
-                         "frac": lds_achieved / LDS_PEAK_GBS if lds_achieved else None,
+                         "frac": lds_achieved / LDS_PEAK_GBS,
                          "traffic": traffic,
                          "lds_bytes": lds_bytes, "lds_bytes_by_class": lds_cls,
                          "lds_rate_B_per_clk_cu": lds_rate,
                          "lds_floor_ms_by_class": lds_floor_ms,
                          "lds_floor_ms": sum(lds_floor_ms.values()),
-                         "passes": n_pass, "chunks": n_chunk, "verified": n_ver,
+                         "executed": {"passes": n_pass, "chunks": n_chunk, "verified": n_ver,
+                                      "lds_bytes_by_class": exe_cls,
+                                      "lds_floor_ms": sum(exe_floor_ms.values()) if n_pass else None,
+                                      "frac": (sum(exe_floor_ms.values()) / topk_ms) if n_pass else None},
                          "venue_skip": bool(eng._ext is not None and eng._ext.s),
                          "half_tiles": bool(eng._ext is not None and eng._ext.half_ent),
                          "avg_launch_ms": topk_ms,

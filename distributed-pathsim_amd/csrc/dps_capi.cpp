@@ -23,6 +23,9 @@ int dps_set_tuning(int32_t key, int32_t value) {
     DPS_REQUIRE(value >= 0 && value <= 2, DPS_ERR_INVALID,
                 "tile build must be 0 (automatic), 1 (block-local) or 2 (global atomics), got %d",
                 value);
+  if (key == DPS_TUNE_BANK_ORDER)
+    DPS_REQUIRE(value >= 0 && value <= 2, DPS_ERR_INVALID,
+                "bank order must be 0 (automatic), 1 (on) or 2 (off), got %d", value);
   dps::g_tune[key].store(value);
   return DPS_OK;
 }

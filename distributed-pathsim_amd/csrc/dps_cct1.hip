@@ -81,40 +81,13 @@ template <> struct Fmt<2> {
 #endif
 constexpr int kEpi1 = DPS_EPI1;                // epilogue blocks read per trip
 
-// Zero the kEpi1 KiB of accumulator an epilogue trip has just read (dwords b0..).
-// DPS_ZERO_ADDTID: ds_write_addtid_b32 (address = M0 + offset + 4 * lane, no
-// address VGPR: 128 B/clk/CU against ~79 for ds_write_b128, MI355X_MICROARCH.md
-// §LDS); M0 is saved and restored inside the statement.  The wave's LDS
-// operations run in order, so the reads issued before it see the old values.
-#ifndef DPS_ZERO_ADDTID
-#define DPS_ZERO_ADDTID 0
-#endif
+// Zero the kEpi1 KiB of accumulator an epilogue trip has just read (dwords
+// b0..).  (ds_write_addtid_b32 zeroes 1.46x faster in isolation,
+// tools/ubench/addtid.hip, but did not move the kernel: DESIGN.md §6.)
 __device__ __forceinline__ void zero_trip(uint32_t* acc, int b0, int lane) {
-#if DPS_ZERO_ADDTID
-  static_assert(kEpi1 == 2, "offsets below cover two 1 KiB blocks");
-  uint32_t save;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "ds_write_addtid_b32 %2 offset:0\n\t"
-      "ds_write_addtid_b32 %2 offset:256\n\t"
-      "ds_write_addtid_b32 %2 offset:512\n\t"
-      "ds_write_addtid_b32 %2 offset:768\n\t"
-      "ds_write_addtid_b32 %2 offset:1024\n\t"
-      "ds_write_addtid_b32 %2 offset:1280\n\t"
-      "ds_write_addtid_b32 %2 offset:1536\n\t"
-      "ds_write_addtid_b32 %2 offset:1792\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(save)
-      : "s"(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(b0 * 4))), "v"(0u)
-      : "memory");
-  (void)acc;
-  (void)lane;
-#else
 #pragma unroll
   for (int i = 0; i < kEpi1; ++i)
     *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
-#endif
 }
 
 // 64 consecutive tiles of one row: lane l describes tile w0 + l.
@@ -288,6 +261,12 @@ __device__ __forceinline__ uint32_t hv_pack(float ratio_up, int slot) {
 }
 __device__ __forceinline__ float hv_ratio(uint32_t hv) { return __uint_as_float(hv); }
 
+// Wave-uniform work counts: candidates completed from the heavy-venue table
+// (counter[3]); profiling build: candidates scored and inserted (counter[15..16]).
+struct WaveCnt {
+  uint32_t ver = 0, cand = 0, ins = 0;
+};
+
 // Candidate queue in VGPRs (no LDS: the wave's 8 KB of LDS is all
 // accumulator, so 20 waves fit a CU): slot s lives in lane s % 64, register
 // s / 64.  Appends come 64 lanes at a time while n < 64, so n < 128.
@@ -322,12 +301,13 @@ __device__ __forceinline__ void vq_push(VQ& Q, bool has, int lab, int m, uint64_
 template <int KPL, bool HV>
 __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& top, int n,
                                          int64_t gx, int lane, int c, uint32_t hv, uint64_t hm,
-                                         uint32_t& nver) {
+                                         WaveCnt& nver) {
   bool cand = lane < n;
   int M = 0, yo = 0;
   double sc = 0.0;
+  nver.cand += static_cast<uint32_t>(n);
   if (HV && hm) {
-    nver += static_cast<uint32_t>(n);
+    nver.ver += static_cast<uint32_t>(n);
     const uint16_t* row = p.hv_c + static_cast<int64_t>(cand ? Q.lab0 : 0) * p.n_hv;
     for (uint64_t m = hm; m; m &= m - 1) {          // wave-uniform, |H| is small
       const int j = __builtin_ctzll(m);
@@ -353,6 +333,7 @@ __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& t
     const double cs = readlane(sc, srcl);
     const int cy = readlane(yo, srcl);
     if (!better(cs, cy, top.kth_s, top.kth_y)) continue;
+    ++nver.ins;
     top.insert(cs, cy, readlane(M, srcl));
   }
 }
@@ -363,7 +344,7 @@ __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& t
 template <int F, int KPL, bool HV>
 __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                           const Stage& S, int lane, int64_t x_lab, int64_t gx,
-                                          int mseg, int c, uint32_t hv, uint64_t hm, uint32_t& nver) {
+                                          int mseg, int c, uint32_t hv, uint64_t hm, WaveCnt& nver) {
   constexpr int kS1 = Fmt<F>::S, kSeg1 = Fmt<F>::SEG;
   const int lnp = S.lnp;
   const int bits = Fmt<F>::BITS << lnp;              // 8..32
@@ -395,21 +376,13 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
   }
 }
 
-// Per-nibble flags (bit 3) of a packed 4-bit dword: nibble >= m, 1 <= m <= 15
-// (no carry leaves a nibble: low3 + 16 - m <= 14).
-__device__ __forceinline__ uint32_t ge_u4(uint32_t a, uint32_t m) {
-  const uint32_t lo = a & 0x77777777u;
-  if (m <= 8u) return (a | (lo + (8u - m) * 0x11111111u)) & 0x88888888u;
-  return (a & (lo + (16u - m) * 0x11111111u)) & 0x88888888u;
-}
-
 // 4-bit epilogue over the whole W = 16384 tile: 8 blocks of 2048 targets (one
 // threshold segment each; lane l reads dwords 4l..4l+3 of the block = targets
 // 32l..32l+31), read and zeroed kEpi1 at a time; candidates queued as in epi1_u8.
 template <int KPL, bool HV>
 __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                         int t, int lane, int64_t x_lab, int64_t gx, int mseg,
-                                        int c, uint32_t hv, uint64_t hm, uint32_t& nver) {
+                                        int c, uint32_t hv, uint64_t hm, WaveCnt& nver) {
   constexpr int kS = Fmt<2>::S, kSeg = Fmt<2>::SEG;
   const int64_t tile_base = static_cast<int64_t>(t) << kS;
   const int64_t xr = x_lab - tile_base;
@@ -421,7 +394,20 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
     const uint32_t pm = (0x10u - (0x80000000u >> __builtin_clz(m))) * 0x11111111u;
     if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) return;
     // target (8*dw + nib) of this lane's 32 -> bit 4*nib + 3 - dw
-    uint32_t F4 = ge_u4(a.x, m) | (ge_u4(a.y, m) >> 1) | (ge_u4(a.z, m) >> 2) | (ge_u4(a.w, m) >> 3);
+    // per-nibble flags (bit 3): nibble >= m, 1 <= m <= 15 (no carry leaves a
+    // nibble: low3 + 16 - m <= 14); m is wave-uniform, so one branch per block
+    // picks the form (per-dword branches cost 2 % of the kernel)
+    uint32_t F4;
+    if (m <= 8u) {
+      const uint32_t K = (8u - m) * 0x11111111u;
+      auto ge = [K](uint32_t v) { return (v | ((v & 0x77777777u) + K)) & 0x88888888u; };
+      F4 = ge(a.x) | (ge(a.y) >> 1) | (ge(a.z) >> 2) | (ge(a.w) >> 3);
+    } else {
+      const uint32_t K = (16u - m) * 0x11111111u;
+      auto ge = [K](uint32_t v) { return (v & ((v & 0x77777777u) + K)) & 0x88888888u; };
+      F4 = ge(a.x) | (ge(a.y) >> 1) | (ge(a.z) >> 2) | (ge(a.w) >> 3);
+    }
+
     const int i0 = (blk << kSeg) + (lane << 5);
     if (xin) {                                     // the source itself never counts
       const int rel = xrel - i0;
@@ -500,7 +486,7 @@ __device__ __forceinline__ void scatter_f(const Batch& B, const Stage& S, uint32
 template <int KPL, bool HV>
 __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                         int t, int lane, int64_t x_lab, int64_t gx, int mseg,
-                                        int c, uint32_t hv, uint64_t hm, uint32_t& nver) {
+                                        int c, uint32_t hv, uint64_t hm, WaveCnt& nver) {
   constexpr int kS1 = Fmt<1>::S, kSeg1 = Fmt<1>::SEG;
   constexpr int kW1 = 1 << kS1;
   const int64_t tile_base = static_cast<int64_t>(t) << kS1;
@@ -670,7 +656,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
   // accumulator passes (each reads and zeroes the 8 KiB accumulator) and 16-byte
   // chunks scattered -- the bench's algorithmic LDS bytes
   uint64_t n_pass = 0, n_chunk = 0;
-  uint32_t n_ver = 0;   // candidates completed from the heavy-venue table (counter[3])
+  WaveCnt n_ver;   // candidates completed from the heavy-venue table, scored, inserted
 
   for (;;) {
     unsigned long long rr = 0;
@@ -919,11 +905,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
   if (lane == 0 && (n_pass | n_chunk)) {
     atomicAdd(p.counter + 1, static_cast<unsigned long long>(n_pass));
     atomicAdd(p.counter + 2, static_cast<unsigned long long>(n_chunk));
-    if (HV && n_ver) atomicAdd(p.counter + 3, static_cast<unsigned long long>(n_ver));
+    if (HV && n_ver.ver) atomicAdd(p.counter + 3, static_cast<unsigned long long>(n_ver.ver));
   }
   if (prof && lane == 0) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) atomicAdd(p.counter + 8 + i, static_cast<unsigned long long>(pc[i]));
+    atomicAdd(p.counter + 15, static_cast<unsigned long long>(n_ver.cand));
+    atomicAdd(p.counter + 16, static_cast<unsigned long long>(n_ver.ins));
   }
 }
 

@@ -182,6 +182,77 @@ __global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__
   }
 }
 
+// Bank order of a bucket's 16-bit entries (both formats: the entry's target
+// dword in the hot kernel's accumulator is entry >> 5, its LDS bank for the
+// 32-lane groups of ds_add_u32 that dword mod 32).  Lane i of a chunk load
+// takes chunk q0 + i, so one scatter instruction adds slot p of 64 consecutive
+// chunks; with the build's (label-ordered) layout those hit a few banks many
+// times.  Here the bucket is sorted by bank and dealt out so that slot p of
+// chunk j holds sorted entry 8 t + p with t = j K mod m (m chunks, K ~ m / 32
+// coprime to m): any 32 consecutive chunks of the bucket then cover the bank
+// range once per slot.  A permutation inside a bucket only: the adds are the
+// same, the sums are the same.  One wave per bucket; buckets above
+// kBankMaxEnt entries keep their order.
+constexpr int kBankMaxEnt = 8192;
+__device__ __forceinline__ int64_t inv_mod(int64_t a, int64_t m) {   // gcd(a, m) == 1
+  int64_t t = 0, nt = 1, r = m, nr = a;
+  while (nr != 0) {
+    const int64_t q = r / nr;
+    int64_t x = t - q * nt; t = nt; nt = x;
+    x = r - q * nr; r = nr; nr = x;
+  }
+  return t < 0 ? t + m : t;
+}
+__device__ __forceinline__ int64_t gcd64(int64_t a, int64_t b) {
+  while (b) { const int64_t r = a % b; a = b; b = r; }
+  return a;
+}
+__global__ __launch_bounds__(kWave) void k_tile_bank_order(const uint32_t* __restrict__ off,
+                                                           int64_t nb, uint32_t* __restrict__ ent) {
+  __shared__ uint16_t src[kBankMaxEnt];
+  __shared__ uint32_t hist[32], cur[32];
+  const int lane = lane_id();
+  uint16_t* e16 = reinterpret_cast<uint16_t*>(ent);
+  for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const int64_t w0 = off[b], w1 = off[b + 1];
+    const int64_t n = 2 * (w1 - w0);                 // entries, a multiple of 8
+    if (n <= 8 || n > kBankMaxEnt) continue;         // one chunk, or too large
+    const int64_t m = n >> 3;
+    if (lane < 32) hist[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (int64_t i = lane; i < n; i += kWave) {
+      const uint16_t e = e16[2 * w0 + i];
+      src[i] = e;
+      atomicAdd(&hist[(e >> 5) & 31u], 1u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane < 32) {
+      const uint32_t h = hist[lane];
+      uint32_t inc = h;
+      for (int d = 1; d < 32; d <<= 1) {
+        const uint32_t o = static_cast<uint32_t>(__shfl_up(static_cast<int>(inc), d, 32));
+        if (lane >= d) inc += o;
+      }
+      cur[lane] = inc - h;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    int64_t K = m / 32 > 1 ? m / 32 : 1;
+    while (gcd64(K, m) != 1) ++K;
+    const int64_t Kinv = inv_mod(K % m, m);
+    for (int64_t i = lane; i < n; i += kWave) {
+      const uint16_t e = src[i];
+      const int64_t si = atomicAdd(&cur[(e >> 5) & 31u], 1u);   // sorted index
+      const int64_t t = si >> 3, p = si & 7;
+      const int64_t j = m == 1 ? 0 : (t * Kinv) % m;           // t = j K mod m
+      e16[2 * w0 + 8 * j + p] = e;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+}
+
 // tile_off in uint32 words (16-bit entries: entry offset / 2, always even).
 __global__ __launch_bounds__(kBlock) void k_tile_off32(const int64_t* __restrict__ p64, int P,
                                                        int64_t n, int wshift,
@@ -764,6 +835,17 @@ int64_t tile_parts(int64_t n_mids, int32_t tile_w) {
   return tile_w > lpb ? tile_w / lpb : 1;
 }
 
+// The bank-order pass over the finished buckets (16-bit entries only).
+int bank_order(bool p16, int64_t nb, const uint32_t* tile_off, uint32_t* tile_ent,
+               hipStream_t st) {
+  const int t = tuning(DPS_TUNE_BANK_ORDER);
+  if (!p16 || nb <= 0 || t != 1) return DPS_OK;
+  const int64_t grid = nb < 65536 ? nb : 65536;
+  k_tile_bank_order<<<static_cast<unsigned>(grid), kWave, 0, st>>>(tile_off, nb, tile_ent);
+  DPS_LAUNCHED();
+  return DPS_OK;
+}
+
 }  // namespace
 }  // namespace dps
 
@@ -926,7 +1008,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
           off64, P, cnt, nb, static_cast<uint32_t>(tile_w) - 1u, fmt, tile_ent);
       DPS_LAUNCHED();
     }
-    return DPS_OK;
+    return bank_order(p16, nb, tile_off, tile_ent, st);
   }
   // many mids: global-atomic counting sort into (v, t) buckets
   DPS_HIP_RET(hipMemsetAsync(cnt, 0, (nb + 1) * sizeof(uint32_t), st));
@@ -955,7 +1037,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
         off64, 1, cursor, nb, static_cast<uint32_t>(tile_w) - 1u, fmt, tile_ent);
     DPS_LAUNCHED();
   }
-  return DPS_OK;
+  return bank_order(p16, nb, tile_off, tile_ent, st);
 }
 
 int dps_walk_row(const int32_t* src_col, const int32_t* src_val, int64_t src_len,

@@ -24,9 +24,10 @@ DEFAULT_TILE_W = 16384
 DEFAULT_SPLIT_ROWS = 256    # heaviest rows of a launch cut into pieces
 DEFAULT_PIECES = 16         # target-tile ranges per split row
 DEFAULT_HEAVY_VENUES = 32   # venue skipping: heavy venues in the dense table (64-byte rows)
-# venue skipping is exact but, on config3, 41 % fewer chunks scattered still
-# took 89.4 ms against 86.9 ms without it (profiles/r03/a): off by default
-DEFAULT_VENUE_SKIP = False
+# venue skipping is exact; on config3 it scatters 41 % fewer chunks: at tile_w
+# 16384 the hot kernel takes 74.1 against 77.9 ms (profiles/r03/d), at 8192
+# 89.4 against 86.9 ms (profiles/r03/a) -- on by default for 16384 only
+VENUE_SKIP_TILE_W = (16384,)
 
 
 def _ptr(t):
@@ -92,7 +93,7 @@ class PathSimEngine:
         # multi-mid SpGEMM: "sort" (expand + segmented sort/unique) or "hash"
         self.spgemm = "sort"
         # venue skipping (dps_venue_skip): exact, row-sum denominator only
-        self.venue_skip = DEFAULT_VENUE_SKIP and denominator == "rowsum"
+        self.venue_skip = tile_w in VENUE_SKIP_TILE_W and denominator == "rowsum"
         self.n_heavy = DEFAULT_HEAVY_VENUES
         # tile_w 16384: the companion 8192-target u8 tiles for wide tiles
         self.half_tiles = True

@@ -77,9 +77,13 @@ const char* dps_last_error(void);
  *   DPS_TUNE_WAVES_PER_ROW  1, 4 or 8 waves share one source row in the hot
  *                           kernel (automatic: 1 for tile_w <= 8192);
  *   DPS_TUNE_TILE_BUILD     1 = block-local, 2 = global-atomic C^T tile build
- *                           (automatic: by the number of mids).
+ *                           (automatic: by the number of mids);
+ *   DPS_TUNE_BANK_ORDER     1 = order each C^T bucket's 16-bit entries for the
+ *                           hot kernel's LDS banks, 2 = keep the build order
+ *                           (automatic: see dps_ct_tiles_build).
  * No reference counterpart (Spark picks its own plans). */
-enum { DPS_TUNE_WAVES_PER_ROW = 1, DPS_TUNE_TILE_BUILD = 2, DPS_TUNE_KEYS = 3 };
+enum { DPS_TUNE_WAVES_PER_ROW = 1, DPS_TUNE_TILE_BUILD = 2, DPS_TUNE_BANK_ORDER = 3,
+       DPS_TUNE_KEYS = 4 };
 int dps_set_tuning(int32_t key, int32_t value);
 int dps_get_tuning(int32_t key);
 /* Number of visible HIP devices (hipGetDeviceCount); < 0 on error. */

@@ -134,3 +134,28 @@ def test_config5_k100_sample_rows():
     co = _oracle(t)
     _check(eng, co, 100, rows=(0, 400))
     _check(eng, co, 100, rows=(2_999_600, 3_000_000))
+
+
+@pytest.mark.parametrize("tile_w", [8192, 16384])
+def test_bank_order_is_a_permutation(tile_w, tune):
+    """dps_set_tuning BANK_ORDER = 1: every C^T bucket holds the
+    same multiset of 16-bit entries, only ordered for the LDS banks, and the
+    top-k is the oracle's."""
+    from dpathsim import _lib
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_dblp
+    t = synth_dblp(20_000, 60_000, 500, seed=7).typed()
+    base = build_engine(t, tile_w=tile_w)
+    tune(_lib.TUNE_BANK_ORDER, 1)
+    eng = build_engine(t, tile_w=tile_w)
+    off = base.tensor("tile_off").cpu().numpy().astype(np.int64)
+    assert np.array_equal(off, eng.tensor("tile_off").cpu().numpy().astype(np.int64))
+    n = int(off[-1]) * 2
+    a = base.tensor("tile_ent").cpu().numpy().view(np.uint16)[:n]
+    b = eng.tensor("tile_ent").cpu().numpy().view(np.uint16)[:n]
+    bucket = np.repeat(np.arange(len(off) - 1), 2 * np.diff(off))
+    ka = np.lexsort((a, bucket))
+    kb = np.lexsort((b, bucket))
+    assert np.array_equal(a[ka], b[kb])          # same entries per bucket
+    assert not np.array_equal(a, b)              # ... in a different order
+    _check(eng, _oracle(t), 10)

@@ -209,6 +209,7 @@ def test_tuning_overrides():
     assert lib.dps_set_tuning(_lib.TUNE_WAVES_PER_ROW, 3) == _lib.DPS_ERR_INVALID
     assert lib.dps_set_tuning(99, 1) == _lib.DPS_ERR_INVALID
     assert lib.dps_set_tuning(_lib.TUNE_TILE_BUILD, 3) == _lib.DPS_ERR_INVALID
+    assert lib.dps_set_tuning(_lib.TUNE_BANK_ORDER, 3) == _lib.DPS_ERR_INVALID
     try:
         assert lib.dps_set_tuning(_lib.TUNE_WAVES_PER_ROW, 4) == 0
         assert lib.dps_get_tuning(_lib.TUNE_WAVES_PER_ROW) == 4

@@ -13,6 +13,10 @@ K = int(os.environ.get("AB_K", str(CONFIGS[cfg][4])))
 # cases "W:NW" (tile width : waves per workgroup, DPATHSIM_NW)
 cases = [tuple(int(v) for v in c.split(":")) for c in os.environ.get("AB_CASES", "32768:4,8192:1").split(",")]
 import dpathsim
+from dpathsim import _lib
+for kv in filter(None, os.environ.get("AB_TUNE", "").split(",")):   # "key=value,..."
+    key, val = (int(v) for v in kv.split("="))
+    _lib.call("dps_set_tuning", key, val)
 t = synth_config(cfg).typed(dpathsim.METAPATHS[CONFIGS[cfg][3]])
 R = int(os.environ.get("AB_ROWS", str(t.n_authors)))
 ref = None
@@ -22,6 +26,10 @@ for W, NW in cases:
         eng = None
         torch.cuda.empty_cache()
         eng, W0 = build_engine(t, tile_w=W), W
+        eng.build(timed=True)
+        ph = eng.info.phase_ms
+        print("  build ms: " + " ".join(f"{k} {v:.3f}" for k, v in ph.items() if k != "host_total")
+              + f" total {sum(v for k, v in ph.items() if k != 'host_total'):.3f}", flush=True)
     os.environ["DPATHSIM_NW"] = str(NW)
     eng.topk(K, 0, min(R, 20000)); torch.cuda.synchronize()
     if True:

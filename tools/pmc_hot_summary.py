@@ -42,7 +42,8 @@ for p in ("fetch", "write", "valu", "lds"):
         c.update({f"{k}@{p}" if k == "GRBM_GUI_ACTIVE" else k: v for k, v in vals.items()})
 W = int(os.environ.get("HOT_W", "16384"))
 rec = {"kernel": f"k_cct1 (dps_cct_topk, W = {W})", "config": "config3", "world": 1, "tile_w": W, "k": 10,
-       "rows": int(os.environ.get("HOT_ROWS", "1000000")), "counters_per_launch": c}
+       "rows": int(os.environ.get("HOT_ROWS", "1000000")),
+       "venue_skip": os.environ.get("HOT_VS", "1" if W == 16384 else "0") == "1", "counters_per_launch": c}
 if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
     rec["hbm_bytes_per_launch"] = 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
     rec["rule"] = "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950: FETCH_SIZE = half of 16-B/lane reads)"
