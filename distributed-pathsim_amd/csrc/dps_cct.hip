@@ -546,6 +546,160 @@ __global__ __launch_bounds__(256) void k_dequeue_list(const uint32_t* __restrict
   }
 }
 
+// ---- symmetric mode (dps_cct_sym) ------------------------------
+// After the band pass (sym = 1): a row is "strong" when its band list holds k
+// positive scores; its k-th score, rounded down to fp32, is the threshold other
+// rows hand pairs on at (tau_emit, by target label; +inf: the row scans every
+// tile itself and takes no records), tau_blk the minimum over 2048 labels.
+// work = the C^T words the rest pass will read for the row plus a fixed cost per
+// accumulator pass (its heavy-first order).
+constexpr int64_t kSymPassCost = 2048;
+__global__ __launch_bounds__(256) void k_sym_plan(
+    int64_t n, int k, int band, int shift, int64_t T, const int32_t* __restrict__ t_rank,
+    const double* __restrict__ band_score, const int64_t* __restrict__ c_ptr,
+    const int32_t* __restrict__ c_col, const uint32_t* __restrict__ tile_off,
+    uint8_t* __restrict__ strong, float* __restrict__ tau_emit, uint32_t* __restrict__ tau_blk,
+    uint32_t* __restrict__ tau_tile, int64_t* __restrict__ work) {
+  for (int64_t x = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; x < n;
+       x += static_cast<int64_t>(gridDim.x) * 256) {
+    const double kth = band_score[x * k + k - 1];
+    const bool st = kth > 0.0;
+    const int64_t lx = t_rank ? t_rank[x] : x;
+    strong[x] = st ? 1 : 0;
+    const float te = st ? __double2float_rd(kth) : __builtin_inff();
+    tau_emit[lx] = te;
+    if (st) {                                    // positive floats order as uints
+      atomicMin(&tau_blk[lx >> 11], __float_as_uint(te));
+      atomicMin(&tau_tile[lx >> shift], __float_as_uint(te));
+    }
+    const int64_t a = lx >> shift;
+    const int64_t t0 = st ? (a + band + 1 < T ? a + band + 1 : T) : 0;
+    int64_t w = 0;
+    for (int64_t j = c_ptr[x]; j < c_ptr[x + 1]; ++j) {
+      const int64_t v = c_col[j];
+      w += static_cast<int64_t>(tile_off[(v + 1) * T]) - static_cast<int64_t>(tile_off[v * T + t0]);
+    }
+    work[x] = w + (T - t0) * kSymPassCost;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_desc_order(const int32_t* __restrict__ t_perm, int64_t n,
+                                                    int32_t* __restrict__ dq) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    dq[i] = t_perm ? t_perm[n - 1 - i] : static_cast<int32_t>(n - 1 - i);
+}
+
+// Records (y <- x, M) grouped by y: counts, then placement.
+__global__ __launch_bounds__(256) void k_rec_count(const int32_t* __restrict__ rec_y,
+                                                   const unsigned long long* __restrict__ rec_n,
+                                                   int64_t cap, uint32_t* __restrict__ cnt) {
+  const int64_t n = static_cast<int64_t>(*rec_n < static_cast<unsigned long long>(cap) ? *rec_n : cap);
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    atomicAdd(&cnt[rec_y[i]], 1u);
+}
+__global__ __launch_bounds__(256) void k_rec_place(const int32_t* __restrict__ rec_y,
+                                                   const int32_t* __restrict__ rec_x,
+                                                   const int32_t* __restrict__ rec_m,
+                                                   const unsigned long long* __restrict__ rec_n,
+                                                   int64_t cap, const int64_t* __restrict__ off,
+                                                   uint32_t* __restrict__ cur, int32_t* __restrict__ sx,
+                                                   int32_t* __restrict__ sm) {
+  const int64_t n = static_cast<int64_t>(*rec_n < static_cast<unsigned long long>(cap) ? *rec_n : cap);
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int32_t y = rec_y[i];
+    const int64_t pos = off[y] + atomicAdd(&cur[y], 1u);
+    sx[pos] = rec_x[i];
+    sm[pos] = rec_m[i];
+  }
+}
+
+// Final lists, one wave per row: weak rows take their rest-pass list (a full
+// scan, zero fill included); strong rows merge their band list (k positive
+// entries, in out_*) with their rest-pass entries (those that beat its k-th)
+// and their records (score recomputed exactly as the hot kernel does).
+template <int KPL>
+__global__ __launch_bounds__(256) void k_sym_merge(
+    int64_t n, int k, const uint8_t* __restrict__ strong, const int64_t* __restrict__ den,
+    const int32_t* __restrict__ r_idx, const int64_t* __restrict__ r_cnt,
+    const double* __restrict__ r_score, const int64_t* __restrict__ off,
+    const int32_t* __restrict__ sx, const int32_t* __restrict__ sm, int32_t* __restrict__ out_idx,
+    int64_t* __restrict__ out_cnt, double* __restrict__ out_score) {
+  const int lane = lane_id();
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * (blockDim.x / kWave);
+  for (int64_t x = wave0; x < n; x += nwaves) {
+    const int64_t base = x * k;
+    if (!strong[x]) {
+      for (int i = lane; i < k; i += kWave) {
+        out_idx[base + i] = r_idx[base + i];
+        out_cnt[base + i] = r_cnt[base + i];
+        out_score[base + i] = r_score[base + i];
+      }
+      continue;
+    }
+    const int64_t rb = off[x], re = off[x + 1];
+    const bool rest = r_idx[base] >= 0;
+    if (!rest && rb == re) continue;             // the band list is the answer
+    TopK<KPL> top;
+    top.init(k);
+#pragma unroll
+    for (int r = 0; r < KPL; ++r) {
+      const int slot = r * kWave + lane;
+      if (slot < k) { top.s[r] = out_score[base + slot]; top.y[r] = out_idx[base + slot];
+                      top.m[r] = static_cast<int>(out_cnt[base + slot]); }
+    }
+    top.filled = k;
+    {
+      const int rk = (k - 1) / kWave, lk = (k - 1) % kWave;
+#pragma unroll
+      for (int r = 0; r < KPL; ++r)
+        if (r == rk) { top.kth_s = readlane(top.s[r], lk); top.kth_y = readlane(top.y[r], lk); }
+    }
+    const int64_t dx = den[x];
+    const int64_t nr = rest ? k : 0;             // rest entries end at the first -1
+    for (int64_t c0 = 0; c0 < nr + (re - rb); c0 += kWave) {
+      const int64_t i = c0 + lane;
+      bool cand = false;
+      double sc = 0.0;
+      int cy = 0, cm = 0;
+      if (i < nr) {
+        cy = r_idx[base + i];
+        if (cy >= 0) { sc = r_score[base + i]; cm = static_cast<int>(r_cnt[base + i]); cand = true; }
+      } else if (i < nr + (re - rb)) {
+        const int64_t j = rb + (i - nr);
+        cy = sx[j];
+        cm = sm[j];
+        sc = static_cast<double>(2 * static_cast<int64_t>(cm)) / static_cast<double>(dx + den[cy]);
+        cand = true;
+      }
+      cand = cand && better(sc, cy, top.kth_s, top.kth_y);
+      uint64_t mask = ballot(cand);
+      while (mask) {
+        const int srcl = __ffsll(static_cast<long long>(mask)) - 1;
+        mask &= mask - 1;
+        const double cs = readlane(sc, srcl);
+        const int y = readlane(cy, srcl);
+        if (!better(cs, y, top.kth_s, top.kth_y)) continue;
+        top.insert(cs, y, readlane(cm, srcl));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < KPL; ++r) {
+      const int slot = r * kWave + lane;
+      if (slot < k) { out_idx[base + slot] = top.y[r]; out_cnt[base + slot] = top.m[r];
+                      out_score[base + slot] = top.s[r]; }
+    }
+  }
+}
+
+// Band-pass work counts added into the rest pass's (kernel_counts reports both).
+__global__ void k_add_counts(const unsigned long long* __restrict__ a, unsigned long long* __restrict__ b) {
+  if (threadIdx.x >= 1 && threadIdx.x < 4) b[threadIdx.x] += a[threadIdx.x];
+}
+
 }  // namespace
 }  // namespace dps
 
@@ -592,6 +746,22 @@ int dps_heavy_first(const int64_t* work, int64_t n_rows, int64_t row_begin, int6
   return DPS_OK;
 }
 
+// Symmetric-mode state of one hot-kernel launch (see CctParams).
+struct SymSetup {
+  int sym, band;
+  const uint8_t* row_strong;
+  const int32_t* seed_idx;
+  const double* seed_score;
+  float* tau_emit;
+  float* tau_blk;
+  float* tau_tile;
+  uint32_t* blk_done;
+  uint32_t* tile_done;
+  int32_t *rec_y, *rec_x, *rec_m;
+  unsigned long long* rec_n;
+  int64_t rec_cap;
+};
+
 static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
                          const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
                          const int32_t* t_rank, int64_t n_targets, int64_t n_mids,
@@ -603,7 +773,7 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
                          size_t ws_bytes, void* stream, int64_t n_pieces = 0,
                          const int32_t* piece_t0 = nullptr, const int32_t* piece_t1 = nullptr,
                          int32_t* piece_idx = nullptr, int64_t* piece_cnt = nullptr,
-                         double* piece_score = nullptr) {
+                         double* piece_score = nullptr, const SymSetup* sy = nullptr) {
   const int shift = log2_exact(tile_w);
   DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED,
               "tile_w must be a power of two in [256, 65536], got %d", tile_w);
@@ -670,6 +840,28 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   p.out_idx = out_idx; p.out_cnt = out_cnt; p.out_score = out_score;
   p.counter = static_cast<unsigned long long*>(ws);
   p.ablate = 0;
+  p.sym = 0;
+  p.band = 0;
+  p.row_strong = nullptr;
+  p.seed_idx = nullptr;
+  p.seed_score = nullptr;
+  p.tau_emit = p.tau_blk = p.tau_tile = nullptr;
+  p.blk_done = p.tile_done = nullptr;
+  p.rec_y = p.rec_x = p.rec_m = nullptr;
+  p.rec_n = nullptr;
+  p.rec_cap = 0;
+  if (sy) {
+    DPS_REQUIRE((shift == 13 || shift == 14) && nw == 1 && !vskip && n_pieces == 0,
+                DPS_ERR_UNSUPPORTED,
+                "symmetric mode runs the one-wave kernel (tile_w 8192 / 16384), no venue "
+                "skipping, no split rows");
+    p.sym = sy->sym; p.band = sy->band; p.row_strong = sy->row_strong;
+    p.seed_idx = sy->seed_idx; p.seed_score = sy->seed_score;
+    p.tau_emit = sy->tau_emit; p.tau_blk = sy->tau_blk; p.tau_tile = sy->tau_tile;
+    p.blk_done = sy->blk_done; p.tile_done = sy->tile_done;
+    p.rec_y = sy->rec_y; p.rec_x = sy->rec_x; p.rec_m = sy->rec_m;
+    p.rec_n = sy->rec_n; p.rec_cap = sy->rec_cap;
+  }
   // Profiling aid only: the production build ignores DPATHSIM_ABLATE (an
   // ablated run returns wrong top-k lists), the -DDPS_PROFILE build honours it.
   if (kProfile)
@@ -744,6 +936,148 @@ int dps_cct_topk_split(const int64_t* c_ptr, const int32_t* c_col, const int32_t
                        tile_off, tile_ent, tile_maxc, tile_gmin, ext, row_begin, n_order,
                        row_order, false, k, out_idx, out_cnt, out_score, ws, ws_bytes, stream, n_pieces,
                        piece_t0, piece_t1, piece_idx, piece_cnt, piece_score);
+}
+
+size_t dps_cct_sym_workspace_size(int64_t n_targets, int32_t k, int64_t rec_cap) {
+  const size_t n = static_cast<size_t>(n_targets > 0 ? n_targets : 1);
+  const size_t nk = n * static_cast<size_t>(k > 0 ? k : 1);
+  const size_t cap = static_cast<size_t>(rec_cap > 0 ? rec_cap : 1);
+  size_t b = 0;
+  b += align_up(nk * 4) + align_up(nk * 8) + align_up(nk * 8);   // rest lists
+  b += align_up(n) + align_up(n * 4) + align_up((n / 2048 + 2) * 4) + align_up(n * 8);
+  b += 2 * align_up((n + 1) * 4) + align_up((n / 2048 + 2) * 4);   // tau_tile, tile_done, blk_done
+  b += align_up(n * 4) + align_up(dps_heavy_first_workspace_size(n_targets));
+  b += 5 * align_up(cap * 4);                                    // records + placed records
+  b += align_up(8) + 2 * align_up((n + 1) * 4) + align_up((n + 1) * 8);
+  b += align_up(scan_workspace_size(n_targets + 1)) + align_up(256);
+  return b + 1024;
+}
+
+int dps_cct_sym(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
+                const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                const uint32_t* tile_off, const uint32_t* tile_ent, const uint32_t* tile_maxc,
+                const int64_t* tile_gmin, const dps_cct_ext* ext, const int32_t* row_order,
+                int32_t band, int64_t rec_cap, int32_t k, int32_t* out_idx, int64_t* out_cnt,
+                double* out_score, unsigned long long* rec_stat, void* sym_ws, size_t sym_ws_bytes,
+                void* ws, size_t ws_bytes, void* stream) {
+  DPS_REQUIRE(band >= 0 && band <= 64, DPS_ERR_INVALID, "band must be in [0, 64]");
+  DPS_REQUIRE(rec_cap >= 1 && rec_cap < (int64_t(1) << 40), DPS_ERR_INVALID, "bad rec_cap");
+  DPS_REQUIRE(k >= 1 && k <= 256, DPS_ERR_UNSUPPORTED, "k must be in [1, 256], got %d", k);
+  DPS_REQUIRE(n_targets >= 0 && n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "bad n_targets");
+  DPS_REQUIRE(rec_stat && out_idx && out_cnt && out_score, DPS_ERR_INVALID, "null output");
+  DPS_REQUIRE(ext == nullptr || ext->s == nullptr, DPS_ERR_UNSUPPORTED,
+              "symmetric mode runs without venue skipping");
+  DPS_REQUIRE(reinterpret_cast<uintptr_t>(sym_ws) % 256 == 0, DPS_ERR_WORKSPACE,
+              "workspace not 256-byte aligned");
+  DPS_REQUIRE(sym_ws_bytes >= dps_cct_sym_workspace_size(n_targets, k, rec_cap),
+              DPS_ERR_WORKSPACE, "cct_sym workspace too small");
+  auto st = static_cast<hipStream_t>(stream);
+  const int64_t n = n_targets;
+  if (n == 0) return DPS_OK;
+  const int shift = log2_exact(tile_w);
+  DPS_REQUIRE(shift == 13 || shift == 14, DPS_ERR_UNSUPPORTED,
+              "symmetric mode needs tile_w 8192 or 16384, got %d", tile_w);
+  const int64_t T = (n + tile_w - 1) / tile_w;
+  const int64_t nk = n * k;
+  Carve c(sym_ws, sym_ws_bytes);
+  int32_t* r_idx = c.take<int32_t>(nk);
+  int64_t* r_cnt = c.take<int64_t>(nk);
+  double* r_score = c.take<double>(nk);
+  uint8_t* strong = c.take<uint8_t>(n);
+  float* tau_emit = c.take<float>(n);
+  uint32_t* tau_blk = c.take<uint32_t>(n / 2048 + 2);
+  uint32_t* tau_tile = c.take<uint32_t>(T + 1);
+  uint32_t* blk_done = c.take<uint32_t>(n / 2048 + 2);
+  uint32_t* tile_done = c.take<uint32_t>(T + 1);
+  int64_t* work = c.take<int64_t>(n);
+  int32_t* dq = c.take<int32_t>(n);
+  const size_t hf_bytes = dps_heavy_first_workspace_size(n);
+  void* hf = c.take<char>(hf_bytes);
+  int32_t* rec_y = c.take<int32_t>(rec_cap);
+  int32_t* rec_x = c.take<int32_t>(rec_cap);
+  int32_t* rec_m = c.take<int32_t>(rec_cap);
+  int32_t* sx = c.take<int32_t>(rec_cap);
+  int32_t* sm = c.take<int32_t>(rec_cap);
+  unsigned long long* rec_n = c.take<unsigned long long>(1);
+  uint32_t* cnt = c.take<uint32_t>(n + 1);
+  uint32_t* cur = c.take<uint32_t>(n + 1);
+  int64_t* off = c.take<int64_t>(n + 1);
+  const size_t scan_ws = scan_workspace_size(n + 1);
+  void* sws = c.take<char>(scan_ws);
+  unsigned long long* band_ctr = c.take<unsigned long long>(32);
+  DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "cct_sym workspace carve failed");
+  {
+    FillSet fs;
+    fs.add(tau_blk, n / 2048 + 2, 0x7F800000u);   // +inf
+    fs.add(tau_tile, T + 1, 0x7F800000u);
+    fs.add(blk_done, n / 2048 + 2, 0u);
+    fs.add(tile_done, T + 1, 0u);
+    fs.add(reinterpret_cast<uint32_t*>(rec_n), 2, 0u);
+    fs.add(cnt, n + 1, 0u);
+    fs.add(cur, n + 1, 0u);
+    DPS_HIP_RET(fill_set(fs, st));
+  }
+  SymSetup sy{};
+  sy.band = band;
+  // 1. band pass: every row over its own tile +- band, into out_*
+  sy.sym = 1;
+  int rc = cct_topk_impl(c_ptr, c_col, c_val, g, g_t, t_perm, t_rank, n, n_mids, tile_w, tile_off,
+                         tile_ent, tile_maxc, tile_gmin, ext, 0, n, row_order, false, k, out_idx,
+                         out_cnt, out_score, band_ctr, 256, stream, 0, nullptr, nullptr, nullptr,
+                         nullptr, nullptr, &sy);
+  if (rc != DPS_OK) return rc;
+  // 2. plan: strong rows, emission thresholds, rest-pass work and order
+  k_sym_plan<<<grid_for(n, 256), 256, 0, st>>>(n, k, band, shift, T, t_rank, out_score, c_ptr,
+                                                 c_col, tile_off, strong, tau_emit, tau_blk,
+                                                 tau_tile, work);
+  DPS_LAUNCHED();
+  // rest pass in descending label order: a row's far targets (higher labels)
+  // have mostly finished and published their own k-th scores by then
+  k_desc_order<<<grid_for(n, 256), 256, 0, st>>>(t_perm, n, dq);
+  DPS_LAUNCHED();
+  (void)hf;
+  (void)hf_bytes;
+  // 3. rest pass: records for the pairs only this row sees
+  sy.sym = 2;
+  sy.row_strong = strong;
+  sy.seed_idx = out_idx;
+  sy.seed_score = out_score;
+  sy.tau_emit = tau_emit;
+  sy.tau_blk = reinterpret_cast<float*>(tau_blk);
+  sy.tau_tile = reinterpret_cast<float*>(tau_tile);
+  sy.blk_done = blk_done;
+  sy.tile_done = tile_done;
+  sy.rec_y = rec_y; sy.rec_x = rec_x; sy.rec_m = rec_m;
+  sy.rec_n = rec_n; sy.rec_cap = rec_cap;
+  rc = cct_topk_impl(c_ptr, c_col, c_val, g, g_t, t_perm, t_rank, n, n_mids, tile_w, tile_off,
+                     tile_ent, tile_maxc, tile_gmin, ext, 0, n, dq, false, k, r_idx, r_cnt, r_score,
+                     ws, ws_bytes, stream, 0, nullptr, nullptr, nullptr, nullptr, nullptr, &sy);
+  if (rc != DPS_OK) return rc;
+  k_add_counts<<<1, 64, 0, st>>>(band_ctr, static_cast<unsigned long long*>(ws));
+  DPS_LAUNCHED();
+  // 4. records grouped by target row, then the final lists
+  k_rec_count<<<grid_for(rec_cap, 256), 256, 0, st>>>(rec_y, rec_n, rec_cap, cnt);
+  DPS_LAUNCHED();
+  DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, off, n + 1, sws, scan_ws, st));
+  k_rec_place<<<grid_for(rec_cap, 256), 256, 0, st>>>(rec_y, rec_x, rec_m, rec_n, rec_cap, off, cur,
+                                                       sx, sm);
+  DPS_LAUNCHED();
+  const unsigned grid = static_cast<unsigned>((n + 3) / 4 < 4096 ? (n + 3) / 4 : 4096);
+  if (k <= 64)
+    k_sym_merge<1><<<grid, 256, 0, st>>>(n, k, strong, g, r_idx, r_cnt, r_score, off, sx, sm,
+                                          out_idx, out_cnt, out_score);
+  else if (k <= 128)
+    k_sym_merge<2><<<grid, 256, 0, st>>>(n, k, strong, g, r_idx, r_cnt, r_score, off, sx, sm,
+                                          out_idx, out_cnt, out_score);
+  else
+    k_sym_merge<4><<<grid, 256, 0, st>>>(n, k, strong, g, r_idx, r_cnt, r_score, off, sx, sm,
+                                          out_idx, out_cnt, out_score);
+  DPS_LAUNCHED();
+  // records emitted (may exceed rec_cap: then the lists are incomplete and the
+  // caller must rerun with a larger capacity)
+  DPS_HIP_RET(hipMemcpyAsync(rec_stat, rec_n, sizeof(unsigned long long), hipMemcpyDeviceToDevice, st));
+  return DPS_OK;
 }
 
 int dps_topk_merge(const int32_t* piece_idx, const int64_t* piece_cnt, const double* piece_score,

@@ -90,12 +90,23 @@ __device__ __forceinline__ void zero_trip(uint32_t* acc, int b0, int lane) {
     *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
 }
 
+// Symmetric rest pass: the bounds other rows raise are read with plain loads
+// (any value read is a valid bound; an atomic load would wait for every
+// outstanding load of the wave, the prefetched chunks included).
+__device__ __forceinline__ float ld_fresh(const float* a) { return *a; }
+__device__ __forceinline__ float wave_min_f32(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
 // 64 consecutive tiles of one row: lane l describes tile w0 + l.
 struct Win1 {
   int w0;          // first tile of the window (wave-uniform)
   uint32_t ub;     // lane: UB of the tile (0xFFFFFFFF = unbounded)
   float gmf;       // lane: smallest g of the tile, as float
   uint64_t live;   // tiles not yet visited that may hold a top-k target
+  uint64_t ykeep;  // symmetric rest pass: tiles that may hold a pair to hand on
   double tau;      // tau the mask was last filtered with
 };
 
@@ -134,21 +145,31 @@ __device__ __forceinline__ uint64_t win_pass(const Win1& w, double tau, float gx
   return ballot(w.ub >= static_cast<uint32_t>(mn));
 }
 
+template <bool SY>
 __device__ __forceinline__ void win_load(const CctParams& p, Win1& w, int w0, int t_lo, int t_end,
                                          int64_t pb, int d, int c, uint32_t vT, int lane,
-                                         double tau, float gxf) {
+                                         double tau, float gxf, int far) {
   w.w0 = w0;
   const int t = w0 + lane;
   w.gmf = t < t_end ? i64_f32(p.tile_gmin[t]) : 0.0f;
   w.ub = win_ub(p, w0, t_end, pb, d, c, vT, lane);
-  w.live = ballot(t >= t_lo && t < t_end && w.ub > 0) & win_pass(w, tau, gxf);
+  w.ykeep = 0;
+  if (SY && far != INT_MAX) {
+    // a far tile stays while its bound reaches the smallest count any of its
+    // targets needs (tau_tile: min tau_emit over the tile)
+    const float ty = t >= far && t < t_end ? ld_fresh(p.tau_tile + t) : __builtin_inff();
+    w.ykeep = ballot(ty < __builtin_inff() &&
+                     w.ub >= static_cast<uint32_t>(max(mneed_lo32(ty, gxf + w.gmf), 1)));
+  }
+  w.live = ballot(t >= t_lo && t < t_end && w.ub > 0) & (win_pass(w, tau, gxf) | w.ykeep);
   w.tau = tau;
 }
 
 // Next tile to process (-1: none left); slides the window as needed.
+template <bool SY>
 __device__ __forceinline__ int next_tile(const CctParams& p, Win1& w, int t_end, int64_t pb, int d,
                                          int c, uint32_t vT, int lane, double tau, float gxf,
-                                         uint32_t& ub_t) {
+                                         uint32_t& ub_t, int far) {
   for (;;) {
     if (w.live) {
       const int b = __builtin_ctzll(w.live);
@@ -157,7 +178,7 @@ __device__ __forceinline__ int next_tile(const CctParams& p, Win1& w, int t_end,
       return w.w0 + b;
     }
     if (w.w0 + kWave >= t_end) return -1;
-    win_load(p, w, w.w0 + kWave, w.w0 + kWave, t_end, pb, d, c, vT, lane, tau, gxf);
+    win_load<SY>(p, w, w.w0 + kWave, w.w0 + kWave, t_end, pb, d, c, vT, lane, tau, gxf, far);
   }
 }
 
@@ -170,17 +191,19 @@ struct Pend1 {
   uint32_t lo, hi;
   uint32_t mx;   // venue skipping: max C[y,v] over the tile's targets (lane = venue)
   int64_t gs;
+  float tb;      // symmetric rest pass, far tile: lane s < 8, min tau_emit over segment s
 };
 
-template <int F, bool HV>
+template <int F, bool HV, bool SY>
 __device__ __forceinline__ void pend_load(const CctParams& p, Pend1& P, int t, uint32_t ub, bool u8h,
-                                          int d0, uint32_t vT, uint32_t vT8, int lane) {
+                                          int d0, uint32_t vT, uint32_t vT8, int lane, int far) {
   P.t = t;
   P.ub = ub;
   P.u8h = u8h;
   P.lo = P.hi = 0;
   P.mx = 0;
   P.gs = 0;
+  P.tb = __builtin_inff();
   if (t < 0) return;
   if (lane < d0) {
     const uint32_t* off = u8h ? p.h_off : p.tile_off;
@@ -193,12 +216,14 @@ __device__ __forceinline__ void pend_load(const CctParams& p, Pend1& P, int t, u
     const int sh = u8h ? Fmt<1>::S : Fmt<F>::S, sg = u8h ? Fmt<1>::SEG : Fmt<F>::SEG;
     const int64_t i = (static_cast<int64_t>(t) << sh) + (static_cast<int64_t>(lane) << sg);
     P.gs = p.g_t[i < p.n_targets ? i : p.n_targets - 1];
+    if (SY && (u8h ? (t >> 1) : t) >= far) P.tb = ld_fresh(p.tau_blk + ((i < p.n_targets ? i : p.n_targets - 1) >> 11));
   }
 }
 
 struct Stage1 {
   Stage S;       // chunk group, tile, pass mode (shared helpers' view)
   float gsf;     // lane s < 8: smallest g of segment s, as float
+  float tbf;     // lane s < 8: symmetric rest pass, min tau_emit of segment s (inf: none)
   bool u8h;      // a u8 half tile of the companion set (F = 2, dual)
   int ubh;       // venue skipping: sum_{h in H} C[x,h] * maxc[h, tile] >= M_H of any target
 };
@@ -225,6 +250,7 @@ __device__ __forceinline__ void stage_make(Stage1& X, const Pend1& P, int c, int
   X.S.nb = (X.S.G.nq + kWave * kU - 1) / (kWave * kU);
   X.S.gq = 0;
   X.gsf = i64_f32(P.gs);
+  X.tbf = P.tb;
 }
 
 // Per-byte flags (bit 7) of a packed u8 dword: byte >= m, for 1 <= m <= 128.
@@ -261,11 +287,51 @@ __device__ __forceinline__ uint32_t hv_pack(float ratio_up, int slot) {
 }
 __device__ __forceinline__ float hv_ratio(uint32_t hv) { return __uint_as_float(hv); }
 
-// Wave-uniform work counts: candidates completed from the heavy-venue table
-// (counter[3]); profiling build: candidates scored and inserted (counter[15..16]).
-struct WaveCnt {
+// Per-row state every candidate flush needs: the wave-uniform work counts
+// (candidates completed from the heavy-venue table, counter[3]; profiling
+// build: candidates scored and inserted, counter[15..16]) and, in the rest pass
+// of the symmetric mode, the row and the first tile whose pairs it hands on.
+struct RowAux {
   uint32_t ver = 0, cand = 0, ins = 0;
+  int x = 0;               // source row (ordinal)
+  int far = INT_MAX;       // sym = 2: targets in tiles >= far may go to records
 };
+
+// Symmetric rest pass, end of row x (label lx): raise tau_emit[lx] to the row's
+// own k-th score (strong rows; it only grows: the band k-th is its floor), then
+// count the row done in its 2048-label block; the block's last row recomputes
+// tau_blk, the tile's last block tau_tile.  No fences: every value another
+// wave may read, stale or fresh, is a valid lower bound (a stale read only
+// loosens a filter), and only the counters must be exact (device atomics).
+template <int KPL>
+__device__ __forceinline__ void sym_publish(const CctParams& p, int64_t lx, bool strong,
+                                            const TopK<KPL>& top, int lane) {
+  if (strong && top.full() && lane == 0) p.tau_emit[lx] = __double2float_rd(top.kth_s);
+  const int64_t b = lx >> 11;
+  const int64_t bsz = p.n_targets - (b << 11) < 2048 ? p.n_targets - (b << 11) : 2048;
+  uint32_t done = 0;
+  if (lane == 0)
+    done = __hip_atomic_fetch_add(p.blk_done + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  done = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(done)));
+  if (done != static_cast<uint32_t>(bsz)) return;
+  float mn = __builtin_inff();
+  for (int64_t i = lane; i < bsz; i += kWave) mn = fminf(mn, ld_fresh(p.tau_emit + (b << 11) + i));
+  mn = wave_min_f32(mn);
+  if (lane == 0) p.tau_blk[b] = mn;
+  const int64_t t = lx >> p.shift;
+  const int per = 1 << (p.shift - 11);                 // blocks per tile
+  const int64_t b0 = t << (p.shift - 11);
+  const int64_t nbt_all = (p.n_targets + 2047) >> 11;
+  const int nbt = static_cast<int>(nbt_all - b0 < per ? nbt_all - b0 : per);
+  uint32_t tdone = 0;
+  if (lane == 0)
+    tdone = __hip_atomic_fetch_add(p.tile_done + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  tdone = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(tdone)));
+  if (tdone != static_cast<uint32_t>(nbt)) return;
+  const float tb = lane < nbt ? ld_fresh(p.tau_blk + b0 + lane) : __builtin_inff();
+  const float tm = wave_min_f32(tb);
+  if (lane == 0) p.tau_tile[t] = tm;
+}
 
 // Candidate queue in VGPRs (no LDS: the wave's 8 KB of LDS is all
 // accumulator, so 20 waves fit a CU): slot s lives in lane s % 64, register
@@ -298,16 +364,16 @@ __device__ __forceinline__ void vq_push(VQ& Q, bool has, int lab, int m, uint64_
 // stages that queued them); their exact share sum_{h in H} C[x,h] * C[y,h]
 // comes from the heavy-venue table (lane h holds C[x,h] in c and the venue's
 // table slot in the low bits of hv, see hv_pack).
-template <int KPL, bool HV>
+template <int KPL, bool HV, bool SY>
 __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& top, int n,
                                          int64_t gx, int lane, int c, uint32_t hv, uint64_t hm,
-                                         WaveCnt& nver) {
+                                         RowAux& ra) {
   bool cand = lane < n;
   int M = 0, yo = 0;
   double sc = 0.0;
-  nver.cand += static_cast<uint32_t>(n);
+  ra.cand += static_cast<uint32_t>(n);
   if (HV && hm) {
-    nver.ver += static_cast<uint32_t>(n);
+    ra.ver += static_cast<uint32_t>(n);
     const uint16_t* row = p.hv_c + static_cast<int64_t>(cand ? Q.lab0 : 0) * p.n_hv;
     for (uint64_t m = hm; m; m &= m - 1) {          // wave-uniform, |H| is small
       const int j = __builtin_ctzll(m);
@@ -316,13 +382,32 @@ __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& t
       if (cand) M += a * static_cast<int>(row[sl]);
     }
   }
+  bool emit = false;
   if (cand) {
     const int64_t label = Q.lab0;
     M += Q.m0;
     yo = p.t_perm ? p.t_perm[label] : static_cast<int>(label);
     const int64_t den = gx + p.g_t[label];
     sc = static_cast<double>(2 * static_cast<int64_t>(M)) / static_cast<double>(den);
+    // symmetric rest pass: a pair in a far tile can enter y's top-k only
+    // through this row (tau_emit <= y's exact band k-th score, rounded down)
+    if (SY && (label >> p.shift) >= ra.far) emit = sc >= static_cast<double>(ld_fresh(p.tau_emit + label));
     cand = better(sc, yo, top.kth_s, top.kth_y);
+  }
+  if (SY && ra.far != INT_MAX) {
+    const uint64_t emk = ballot(emit);
+    if (emk) {
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(p.rec_n, static_cast<unsigned long long>(__popcll(emk)));
+      base = (static_cast<unsigned long long>(readlane(static_cast<int>(base >> 32), 0)) << 32) |
+             static_cast<uint32_t>(readlane(static_cast<int>(base), 0));
+      const unsigned long long slot = base + static_cast<unsigned long long>(mbcnt(emk));
+      if (emit && slot < static_cast<unsigned long long>(p.rec_cap)) {
+        p.rec_y[slot] = yo;
+        p.rec_x[slot] = ra.x;
+        p.rec_m[slot] = M;
+      }
+    }
   }
   if (n >= kWave) { Q.lab0 = Q.lab1; Q.m0 = Q.m1; }
   Q.n -= n;
@@ -333,7 +418,7 @@ __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& t
     const double cs = readlane(sc, srcl);
     const int cy = readlane(yo, srcl);
     if (!better(cs, cy, top.kth_s, top.kth_y)) continue;
-    ++nver.ins;
+    ++ra.ins;
     top.insert(cs, cy, readlane(M, srcl));
   }
 }
@@ -341,10 +426,10 @@ __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& t
 // u16 / u32 pass epilogue (UB > 255, rare): scan + zero the accumulator of
 // pass `pass` (2 or 1 targets per dword), queue targets reaching their
 // segment's threshold.
-template <int F, int KPL, bool HV>
+template <int F, int KPL, bool HV, bool SY>
 __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                           const Stage& S, int lane, int64_t x_lab, int64_t gx,
-                                          int mseg, int c, uint32_t hv, uint64_t hm, WaveCnt& nver) {
+                                          int mseg, int c, uint32_t hv, uint64_t hm, RowAux& ra) {
   constexpr int kS1 = Fmt<F>::S, kSeg1 = Fmt<F>::SEG;
   const int lnp = S.lnp;
   const int bits = Fmt<F>::BITS << lnp;              // 8..32
@@ -371,7 +456,7 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
       const uint64_t mk = ballot(cand);
       if (!mk) continue;
       vq_push(Q, cand, static_cast<int>(label), static_cast<int>(M), mk, lane);
-      if (Q.n >= kWave) vq_flush<KPL, HV>(p, Q, top, kWave, gx, lane, c, hv, hm, nver);
+      if (Q.n >= kWave) vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
     }
   }
 }
@@ -379,10 +464,10 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
 // 4-bit epilogue over the whole W = 16384 tile: 8 blocks of 2048 targets (one
 // threshold segment each; lane l reads dwords 4l..4l+3 of the block = targets
 // 32l..32l+31), read and zeroed kEpi1 at a time; candidates queued as in epi1_u8.
-template <int KPL, bool HV>
+template <int KPL, bool HV, bool SY>
 __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                         int t, int lane, int64_t x_lab, int64_t gx, int mseg,
-                                        int c, uint32_t hv, uint64_t hm, WaveCnt& nver) {
+                                        int c, uint32_t hv, uint64_t hm, RowAux& ra) {
   constexpr int kS = Fmt<2>::S, kSeg = Fmt<2>::SEG;
   const int64_t tile_base = static_cast<int64_t>(t) << kS;
   const int64_t xr = x_lab - tile_base;
@@ -430,7 +515,7 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
         mv = static_cast<int>((wv >> (nib * 4)) & 0xFu);
       }
       vq_push(Q, has, lab, mv, mk, lane);
-      if (Q.n >= kWave) vq_flush<KPL, HV>(p, Q, top, kWave, gx, lane, c, hv, hm, nver);
+      if (Q.n >= kWave) vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
     }
   };
 #pragma unroll 1
@@ -483,10 +568,10 @@ __device__ __forceinline__ void scatter_f(const Batch& B, const Stage& S, uint32
 // u8 epilogue over the whole tile: 8 blocks of 1024 targets (one threshold
 // segment each, lane l reads dwords 4l..4l+3 of the block), read and zeroed 4
 // at a time; candidates are queued and scored 64 at a time by flush().
-template <int KPL, bool HV>
+template <int KPL, bool HV, bool SY>
 __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                         int t, int lane, int64_t x_lab, int64_t gx, int mseg,
-                                        int c, uint32_t hv, uint64_t hm, WaveCnt& nver) {
+                                        int c, uint32_t hv, uint64_t hm, RowAux& ra) {
   constexpr int kS1 = Fmt<1>::S, kSeg1 = Fmt<1>::SEG;
   constexpr int kW1 = 1 << kS1;
   const int64_t tile_base = static_cast<int64_t>(t) << kS1;
@@ -531,7 +616,7 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
         mv = static_cast<int>((wv >> (byte * 8)) & 0xFFu);
       }
       vq_push(Q, has, lab, mv, mk, lane);
-      if (Q.n >= kWave) vq_flush<KPL, HV>(p, Q, top, kWave, gx, lane, c, hv, hm, nver);
+      if (Q.n >= kWave) vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
     }
   };
 #pragma unroll 1
@@ -635,8 +720,14 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
 #ifndef DPS_W5_KPL
 #define DPS_W5_KPL 1
 #endif
-template <int F, int KPL, bool HV>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DPS_W5_KPL ? 5 : 4))) void k_cct1(CctParams p) {
+template <int F, int KPL, bool HV, bool SY>
+// The symmetric-mode instantiation carries the record path and the published
+// bounds: DPS_SYM_WPE waves per SIMD (4: 128 VGPRs, no spills).
+#ifndef DPS_SYM_WPE
+#define DPS_SYM_WPE 4
+#endif
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
+    SY ? DPS_SYM_WPE : KPL <= DPS_W5_KPL ? 5 : 4))) void k_cct1(CctParams p) {
   // LDS: the accumulator at address 0 (scatter ORs the in-tile offset into 0)
   // then the candidate queue.
   __shared__ __attribute__((aligned(16))) uint32_t lds[kAcc1];
@@ -656,7 +747,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
   // accumulator passes (each reads and zeroes the 8 KiB accumulator) and 16-byte
   // chunks scattered -- the bench's algorithmic LDS bytes
   uint64_t n_pass = 0, n_chunk = 0;
-  WaveCnt n_ver;   // candidates completed from the heavy-venue table, scored, inserted
+  RowAux ra;       // work counts; the symmetric mode's row state
 
   for (;;) {
     unsigned long long rr = 0;
@@ -666,8 +757,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
     const int64_t x = p.row_order ? static_cast<int64_t>(p.row_order[r]) : p.row_begin + r;
     const bool is_piece = r < p.n_pieces;
     const int64_t ro = (is_piece || p.out_by_slot) ? r : x - p.row_begin;
-    const int t_beg = is_piece ? p.piece_t0[r] : 0;
-    const int t_end = is_piece ? p.piece_t1[r] : static_cast<int>(p.T);
+    int t_beg = is_piece ? p.piece_t0[r] : 0;
+    int t_end = is_piece ? p.piece_t1[r] : static_cast<int>(p.T);
     DPS_DASSERT(0 <= t_beg && t_beg <= t_end && t_end <= p.T);
     const int64_t x_lab = p.t_rank ? static_cast<int64_t>(p.t_rank[x]) : x;
     const int64_t pb = p.c_ptr[x];
@@ -676,6 +767,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
     const float gxf = i64_f32(gx);
     TopK<KPL> top;
     top.init(p.k);
+    ra.x = static_cast<int>(x);
+    ra.far = INT_MAX;
+    bool strong = false;                // sym rest pass: a partial list, no zero fill
+    if (SY) {
+      const int a = static_cast<int>(x_lab >> p.shift);
+      if (p.sym == 1) {                 // band pass: the row's own tile +- band
+        t_beg = max(t_beg, a - p.band);
+        t_end = min(t_end, a + p.band + 1);
+      } else {                          // rest pass
+        ra.far = a + p.band + 1;
+        strong = p.row_strong[x] != 0;
+        if (strong) {                   // tiles above the band, its k-th as the floor
+          const int64_t e = x * p.k + p.k - 1;
+          top.set_floor(p.seed_score[e], p.seed_idx[e]);
+          t_beg = max(t_beg, ra.far);
+        }
+      }
+    }
 
     if (d > 0 && t_beg < t_end) {
       const int d0 = d < kWave ? d : kWave;
@@ -713,7 +822,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
           h_next = -1;
           return;
         }
-        tn = next_tile(p, w, t_end, pb, d, c, vT, lane, tau, gxf, ubn);
+        tn = next_tile<SY>(p, w, t_end, pb, d, c, vT, lane, tau, gxf, ubn, ra.far);
         if (!dual || tn < 0 || ubn <= Fmt<F>::UB0) return;
         const int ta = 2 * tn, tb = 2 * tn + 1;
         const uint32_t ua = half_ub(ta, ubn);
@@ -738,14 +847,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
           hv = hv_pack(static_cast<float>(static_cast<double>(c) / static_cast<double>(p.s[v])) *
                            (1.0f + 0x1p-20f), sl);
       }
-      win_load(p, w, t_beg, t_beg, t_end, pb, d, c, vT, lane, -1.0, gxf);
+      win_load<SY>(p, w, t_beg, t_beg, t_end, pb, d, c, vT, lane, -1.0, gxf, ra.far);
       uint32_t ub_t = 0;
       int t0;
       bool u8n;
       choose(-1.0, t0, ub_t, u8n);
       if (t0 >= 0) {
         Pend1 P;
-        pend_load<F, HV>(p, P, t0, ub_t, u8n, d0, vT, vT8, lane);
+        pend_load<F, HV, SY>(p, P, t0, ub_t, u8n, d0, vT, vT8, lane, ra.far);
         Stage1 X;
         stage_make<F>(X, P, c, d0, 0ull, lane);
         bool hchg = false;        // H grew at the last stage boundary
@@ -753,7 +862,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
         issue1(X.S, 0, X.u8h ? p.h_ent : p.tile_ent, lane, B);
         int t1;
         choose(-1.0, t1, ub_t, u8n);
-        pend_load<F, HV>(p, P, t1, ub_t, u8n, d0, vT, vT8, lane);
+        pend_load<F, HV, SY>(p, P, t1, ub_t, u8n, d0, vT, vT8, lane, ra.far);
         for (;;) {
           const int npass = 1 << X.S.lnp;
           bool more = false;
@@ -775,7 +884,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
             // score what is queued while the list is filling or the queue is
             // half full (one memory round trip per 64 candidates)
             if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
-              vq_flush<KPL, HV>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane, c, hv, hm, n_ver);
+              vq_flush<KPL, HV, SY>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane, c, hv, hm, ra);
             const double tau = top.full() ? top.kth_s : -1.0;
             int mseg = 1;
             if (tau > 0.0) {
@@ -799,6 +908,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
                 mseg = mn > 1 ? mn : 1;
               }
             }
+            if (SY && X.tbf < __builtin_inff()) {
+              // symmetric rest pass, far tile: also every count that can reach the
+              // segment's smallest tau_emit (pairs this row hands on)
+              const int my = mneed_lo32(X.tbf, gxf + X.gsf);
+              mseg = min(mseg, my > 1 ? my : 1);
+            }
             const bool last = X.S.pass + 1 == npass;
             Stage S = X.S;
             const bool u8S = F == 1 || X.u8h;   // this stage's counters: u8 format
@@ -810,7 +925,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
               bool row_done = false;
               hchg = false;
               if (tau > w.tau) {
-                w.live &= win_pass(w, tau, gxf);
+                w.live &= win_pass(w, tau, gxf) | w.ykeep;
                 w.tau = tau;
                 if (HV) {
                   // H = the heavy venues with C[x,h] / s_h <= tau / 2 (hr is an
@@ -831,26 +946,26 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
               if (prof) ts[6] = __builtin_amdgcn_s_memtime();
               int tn = -1;
               if (more) choose(tau, tn, ub_t, u8n);
-              pend_load<F, HV>(p, P, tn, ub_t, u8n, d0, vT, vT8, lane);
+              pend_load<F, HV, SY>(p, P, tn, ub_t, u8n, d0, vT, vT8, lane, ra.far);
             }
             if (prof) ts[3] = __builtin_amdgcn_s_memtime();
             if (S.lnp == 0) {
               if (u8S)
-                epi1_u8<KPL, HV>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
-                                 hmS, n_ver);
+                epi1_u8<KPL, HV, SY>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
+                                 hmS, ra);
               else
-                epi1_u4<KPL, HV>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
-                                 hmS, n_ver);
+                epi1_u4<KPL, HV, SY>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
+                                 hmS, ra);
             } else if (u8S) {
-              epi1_wide<1, KPL, HV>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, n_ver);
+              epi1_wide<1, KPL, HV, SY>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, ra);
             } else {
-              epi1_wide<F, KPL, HV>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, n_ver);
+              epi1_wide<F, KPL, HV, SY>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, ra);
             }
             // the queue holds counts that miss hmS: complete them before the
             // next stage's (larger) H applies
             if (HV && hchg)
               while (Q.n > 0)
-                vq_flush<KPL, HV>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane, c, hv, hmS, n_ver);
+                vq_flush<KPL, HV, SY>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane, c, hv, hmS, ra);
             if (prof) {
               ts[4] = __builtin_amdgcn_s_memtime();
 #pragma unroll
@@ -863,7 +978,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
           if (!more) break;
         }
       }
-      while (Q.n > 0) vq_flush<KPL, HV>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane, c, hv, hm, n_ver);
+      while (Q.n > 0) vq_flush<KPL, HV, SY>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane, c, hv, hm, ra);
     }
 
     // ranked entries, then zero-score targets in reference order, then -1
@@ -876,7 +991,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
       if (slot < top.filled) { oi[slot] = top.y[q]; oc[slot] = top.m[q]; os[slot] = top.s[q]; }
     }
     const int64_t avail = p.n_targets - 1;
-    const int want = is_piece ? top.filled : static_cast<int>(avail < p.k ? avail : p.k);
+    const int want = (is_piece || strong) ? top.filled : static_cast<int>(avail < p.k ? avail : p.k);
     int slot = top.filled;
     for (int64_t yb = 0; slot < want && yb < p.n_targets; yb += kWave) {
       const int64_t yc = yb + lane;
@@ -901,17 +1016,18 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(KPL <= DP
       oc[s2] = 0;
       os[s2] = 0.0;
     }
+    if (SY && p.sym == 2) sym_publish<KPL>(p, x_lab, strong, top, lane);
   }
   if (lane == 0 && (n_pass | n_chunk)) {
     atomicAdd(p.counter + 1, static_cast<unsigned long long>(n_pass));
     atomicAdd(p.counter + 2, static_cast<unsigned long long>(n_chunk));
-    if (HV && n_ver.ver) atomicAdd(p.counter + 3, static_cast<unsigned long long>(n_ver.ver));
+    if (HV && ra.ver) atomicAdd(p.counter + 3, static_cast<unsigned long long>(ra.ver));
   }
   if (prof && lane == 0) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) atomicAdd(p.counter + 8 + i, static_cast<unsigned long long>(pc[i]));
-    atomicAdd(p.counter + 15, static_cast<unsigned long long>(n_ver.cand));
-    atomicAdd(p.counter + 16, static_cast<unsigned long long>(n_ver.ins));
+    atomicAdd(p.counter + 15, static_cast<unsigned long long>(ra.cand));
+    atomicAdd(p.counter + 16, static_cast<unsigned long long>(ra.ins));
   }
 }
 
@@ -921,14 +1037,16 @@ int launch1(const CctParams& p, hipStream_t st) {
   DPS_HIP_RET(hipGetDevice(&dev));
   DPS_HIP_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
   int wpc = KPL <= DPS_W5_KPL ? 20 : 16;   // 5 or 4 waves per SIMD, 8 KB of LDS each
+  if (p.sym) wpc = 4 * (DPS_SYM_WPE < (KPL <= DPS_W5_KPL ? 5 : 4) ? DPS_SYM_WPE : (KPL <= DPS_W5_KPL ? 5 : 4));
 #ifdef DPS_PROFILE
   if (const char* e = std::getenv("DPATHSIM_LEAN_WPC")) wpc = std::atoi(e);   // experiments
   if (wpc < 1 || wpc > 20) wpc = 20;
 #endif
   int64_t grid = static_cast<int64_t>(n_cu) * wpc;
   if (grid > p.n_rows) grid = p.n_rows;
-  if (p.hv_c) k_cct1<F, KPL, true><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
-  else k_cct1<F, KPL, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  if (p.sym) k_cct1<F, KPL, false, true><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  else if (p.hv_c) k_cct1<F, KPL, true, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  else k_cct1<F, KPL, false, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
   DPS_LAUNCHED();
   return DPS_OK;
 }

@@ -60,6 +60,38 @@ struct CctParams {
   const uint32_t* h_ent;
   const uint32_t* h_maxc;
   int64_t T8;
+  // symmetric mode (lean kernel, dps_cct_sym): M[x,y] = M[y,x],
+  // so a pair is scanned once.  Row x in tile a = label(x) >> shift:
+  //   sym = 1  band pass: tiles [a - band, a + band] only;
+  //   sym = 2  rest pass: "strong" rows (row_strong[x]) scan tiles > a + band
+  //            only, with their band list's k-th entry (seed_*[x * k + k - 1])
+  //            as the threshold floor, and list what beats it (no zero fill);
+  //            the others scan every tile from scratch.  A pair with tile(y) >
+  //            a + band is seen by x alone: x hands it to y as a record
+  //            (rec_y = y, rec_x = x, rec_m = M) when its score reaches
+  //            tau_emit[label(y)] (a lower bound of y's k-th score; +inf for
+  //            rows that scan everything themselves); tau_blk[label >> 11] is
+  //            the minimum of tau_emit over 2048 labels (the epilogue filter),
+  //            tau_tile over a tile (which tiles a row may not skip).  Rows
+  //            run in descending label order and, when done, raise tau_emit
+  //            to their own k-th score; the last row of a block (of a tile)
+  //            recomputes tau_blk (tau_tile).  Every value any reader sees is
+  //            a lower bound of the row's final k-th score.
+  int sym;
+  int band;
+  const uint8_t* row_strong;
+  const int32_t* seed_idx;
+  const double* seed_score;
+  float* tau_emit;
+  float* tau_blk;
+  float* tau_tile;           // min tau_emit over each tile (tile skipping)
+  uint32_t* blk_done;        // rows finished per 2048-label block (rest pass)
+  uint32_t* tile_done;       // blocks finished per tile
+  int32_t* rec_y;
+  int32_t* rec_x;
+  int32_t* rec_m;
+  unsigned long long* rec_n;
+  int64_t rec_cap;
 };
 
 // Lean one-wave kernel for W = 8192 (dps_cct1.hip).
@@ -140,6 +172,7 @@ struct TopK {
   int filled;
   double kth_s;
   int kth_y;
+  bool floored;
 
   __device__ void init(int k_) {
 #pragma unroll
@@ -148,8 +181,17 @@ struct TopK {
     filled = 0;
     kth_s = -1.0;
     kth_y = INT_MAX;
+    floored = false;
   }
-  __device__ bool full() const { return filled == k; }
+  __device__ bool full() const { return filled == k || floored; }
+  // Threshold floor (symmetric rest pass): the row's k-th score so far is at
+  // least (fs, fy) -- its band list's k-th -- although this list starts empty;
+  // kth stays at the floor until k entries beat it.
+  __device__ void set_floor(double fs, int fy) {
+    kth_s = fs;
+    kth_y = fy;
+    floored = true;
+  }
   // Insert a candidate known to beat the k-th entry (wave-uniform arguments).
   __device__ void insert(double cs, int cy, int cm) {
     const int lane = lane_id();
@@ -184,6 +226,7 @@ struct TopK {
       else if (slot == pos) { s[r] = cs; y[r] = cy; m[r] = cm; }
     }
     filled = filled < k ? filled + 1 : k;
+    if (floored && filled < k) return;   // the floor stays the threshold
     const int rk = (k - 1) / kWave, lk = (k - 1) % kWave;
 #pragma unroll
     for (int r = 0; r < KPL; ++r)

@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPATHSIM_LIB", os.path.join(_HERE, "libdpathsim.so"))
 
-ABI_VERSION = 2  # DPS_ABI_VERSION in include/dpathsim.h
+ABI_VERSION = 3  # DPS_ABI_VERSION in include/dpathsim.h
 
 DPS_OK = 0
 DPS_ERR_INVALID = -1
@@ -87,6 +87,9 @@ SIGNATURES = {
     "dps_cct_topk_split": (C.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p,
                                      _p, _p, _i64, _i64, _p, _i64, _p, _p, _i64, _p, _p, _p, _i32,
                                      _p, _p, _p, _p, _sz, _p]),
+    "dps_cct_sym_workspace_size": (_sz, [_i64, _i32, _i64]),
+    "dps_cct_sym": (C.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p,
+                              _p, _i32, _i64, _i32, _p, _p, _p, _p, _p, _sz, _p, _sz, _p]),
     "dps_heavy_venues": (C.c_int, [_p, _i64, _i32, _p, _p]),
     "dps_heavy_table": (C.c_int, [_p, _p, _p, _p, _i64, _p, _i32, _p, _p]),
     "dps_set_tuning": (C.c_int, [_i32, _i32]),

@@ -28,6 +28,9 @@ DEFAULT_HEAVY_VENUES = 32   # venue skipping: heavy venues in the dense table (6
 # 16384 the hot kernel takes 74.1 against 77.9 ms (profiles/r03/d), at 8192
 # 89.4 against 86.9 ms (profiles/r03/a) -- on by default for 16384 only
 VENUE_SKIP_TILE_W = (16384,)
+SYM_TILE_W = (8192, 16384)
+DEFAULT_SYM_BAND = 1          # tiles either side of a row's own scanned by both rows
+DEFAULT_SYM_REC_PER_ROW = 32  # record capacity per row (config3: about 5 per row needed)
 
 
 def _ptr(t):
@@ -98,6 +101,13 @@ class PathSimEngine:
         # tile_w 16384: the companion 8192-target u8 tiles for wide tiles
         self.half_tiles = True
         self._ext = None
+        # symmetric mode (dps_cct_sym): every pair scanned once; whole-range
+        # launches at tile_w 8192 / 16384 (venue skipping does not apply there)
+        self.sym = False
+        self.sym_band = DEFAULT_SYM_BAND
+        self.sym_rec_per_row = DEFAULT_SYM_REC_PER_ROW
+        self.defer_checks = False
+        self._sym_stat = None
         # load balance of the hot kernel: the split_rows heaviest rows of a
         # launch are cut into `pieces` target-tile ranges (see topk())
         self.split_rows = DEFAULT_SPLIT_ROWS
@@ -429,6 +439,8 @@ class PathSimEngine:
         idx, cnt, sc = out
         if R == 0:
             return idx, cnt, sc
+        if self.sym and self.tile_w in SYM_TILE_W and row_begin == 0 and row_end == NA:
+            return self._topk_sym(k, out)
         T = max(1, math.ceil(NA / self.tile_w))
         M = self.split_rows if split_rows is None else int(split_rows)
         P = min(self.pieces if pieces is None else int(pieces), T, 64)
@@ -472,6 +484,54 @@ class PathSimEngine:
             _lib.call("dps_topk_merge", _ptr(pbuf[0]), _ptr(pbuf[1]), _ptr(pbuf[2]), _ptr(dq), M,
                       P, int(k), NA, int(row_begin), _ptr(idx), _ptr(cnt), _ptr(sc), self.stream)
         return idx, cnt, sc
+
+    def _topk_sym(self, k, out, cap=None):
+        """dps_cct_sym over every row: the band pass in heavy-first order, then
+        the library's own plan, rest pass and merge.  The records emitted are
+        checked against the capacity here (one synchronisation), or by
+        :meth:`check_sym` when ``defer_checks`` is set; an overflow reruns with
+        room for all of them."""
+        d = self._dev
+        NA = self.typed.n_authors
+        idx, cnt, sc = out
+        cap = int(cap or max(1, int(self.sym_rec_per_row * NA)))
+        with torch.cuda.device(self.device):
+            dq = torch.empty(NA, dtype=torch.int32, device=self.device)
+            hws = self._ws(_lib.size("dps_heavy_first_workspace_size", NA))
+            _lib.call("dps_heavy_first", _ptr(d["row_terms"][:NA]), NA, 0, 0, 1, _ptr(dq), _ptr(hws),
+                      hws.numel(), self.stream)
+            sws = self._ws(_lib.size("dps_cct_sym_workspace_size", NA, k, cap))
+            stat = torch.zeros(1, dtype=torch.int64, device=self.device)
+            if self._ext is not None and self._ext.half_ent:
+                self._ext_sym = _lib.CctExt(None, None, None, 0, self._ext.half_off,
+                                            self._ext.half_ent, self._ext.half_maxc)
+                ext = C.addressof(self._ext_sym)
+            else:
+                ext = None
+            _lib.call("dps_cct_sym", _ptr(d["c_ptr"]), _ptr(d["c_col"]), _ptr(d["c_val"]),
+                      _ptr(d["den"]), _ptr(d["g_t"]), _ptr(d["t_perm"]), _ptr(d["t_rank"]), NA,
+                      self.typed.n_mids, self.tile_w, _ptr(d["tile_off"]), _ptr(d["tile_ent"]),
+                      _ptr(d["tile_maxc"]) if self.tile_skip else None, _ptr(d["tile_gmin"]), ext,
+                      _ptr(dq), int(self.sym_band), cap, int(k), _ptr(idx), _ptr(cnt), _ptr(sc),
+                      _ptr(stat), _ptr(sws), sws.numel(), _ptr(d["topk_ws"]), d["topk_ws"].numel(),
+                      self.stream)
+            self._sym_stat = (stat, cap, k)
+            if not self.defer_checks:
+                n_rec = int(stat.item())
+                if n_rec > cap:
+                    return self._topk_sym(k, out, cap=n_rec + n_rec // 4 + 1024)
+        return idx, cnt, sc
+
+    def check_sym(self):
+        """Records of the last symmetric launch within capacity (else raise)."""
+        if self._sym_stat is None:
+            return 0
+        stat, cap, _ = self._sym_stat
+        n_rec = int(stat.item())
+        if n_rec > cap:
+            raise RuntimeError(f"symmetric top-k: {n_rec} records exceed the capacity {cap}; "
+                               "raise sym_rec_per_row")
+        return n_rec
 
     def topk_rows(self, k: int, rows, out=None):
         """★ top-k of an arbitrary list of author rows (device or host int array),

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define DPS_ABI_VERSION 2
+#define DPS_ABI_VERSION 3
 
 enum {
   DPS_OK = 0,
@@ -410,6 +410,37 @@ int dps_topk_merge(const int32_t* piece_idx, const int64_t* piece_cnt, const dou
                    const int32_t* rows, int64_t n_groups, int32_t pieces_per_row, int32_t k,
                    int64_t n_targets, int64_t row_begin, int32_t* out_idx, int64_t* out_cnt,
                    double* out_score, void* stream);
+
+/* ★ Symmetric all-pairs top-k: the same lists as dps_cct_topk over every row
+ * [0, n_targets), with each pair (x, y) scanned once instead of twice (M[x,y] =
+ * M[y,x], the score's denominator is symmetric too).  Targets are labelled by
+ * ascending g and cut into tiles of tile_w (8192 or 16384; one-wave kernel, no
+ * venue skipping).  Row x in tile a:
+ *   1. band pass: x over the tiles [a - band, a + band] (heavy-first order
+ *      row_order, may be NULL), its band list into out_*;
+ *   2. rows whose band list holds k positive scores ("strong") continue over
+ *      the tiles above a + band with the band's k-th score as the threshold;
+ *      the others scan every tile.  A pair with y in a tile above a + band is
+ *      seen by x alone: it becomes a record (y <- x, M) when its score reaches
+ *      y's band k-th score (rounded down to fp32), which bounds y's final k-th
+ *      score from below, so no pair of y's top-k is lost;
+ *   3. each strong row's band list, rest-pass list and records merge into its
+ *      exact top-k (order score desc, then target ordinal asc).
+ * rec_cap bounds the records (workspace: dps_cct_sym_workspace_size); the
+ * number emitted is written to *rec_stat (device) -- above rec_cap the lists
+ * are incomplete and the call must be repeated with a larger rec_cap.  ws is
+ * dps_cct_topk's counter workspace (words 1-3: both passes' counts).
+ * Replaces the same reference loop as dps_cct_topk (DPathSim_APVPA.py:36,
+ * 90-109, 51-52). */
+size_t dps_cct_sym_workspace_size(int64_t n_targets, int32_t k, int64_t rec_cap);
+int dps_cct_sym(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                const int64_t* g, const int64_t* g_t, const int32_t* t_perm,
+                const int32_t* t_rank, int64_t n_targets, int64_t n_mids, int32_t tile_w,
+                const uint32_t* tile_off, const uint32_t* tile_ent, const uint32_t* tile_maxc,
+                const int64_t* tile_gmin, const dps_cct_ext* ext, const int32_t* row_order,
+                int32_t band, int64_t rec_cap, int32_t k, int32_t* out_idx, int64_t* out_cnt,
+                double* out_score, unsigned long long* rec_stat, void* sym_ws, size_t sym_ws_bytes,
+                void* ws, size_t ws_bytes, void* stream);
 
 /* Heavy-first dequeue list for dps_cct_topk / dps_cct_topk_split (no
  * counterpart in the reference; load balance of the all-pairs loop :36):

@@ -25,7 +25,7 @@ def test_header_symbols_exported():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(_lib.exported_symbols()) == declared
-    assert lib.dps_abi_version() == 2
+    assert lib.dps_abi_version() == 3
 
 
 def test_no_cpu_fallback_when_library_missing(monkeypatch):
