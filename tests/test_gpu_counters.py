@@ -27,6 +27,7 @@ def test_lean_counters_without_tile_skipping(tile_w, half, npass):
     t = synth_dblp(40_000, 120_000, 500, seed=7).typed()
     eng = PathSimEngine(t, tile_w=tile_w)
     eng.half_tiles = half
+    eng.venue_skip = False          # every bucket of the row's venues is scattered
     eng.upload().build()
     na, nv = t.n_authors, t.n_mids
     tw = 8192 if half else tile_w
