@@ -46,7 +46,8 @@ def parse():
     ap.add_argument("--config", default="config3")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink authors/papers (debug)")
     ap.add_argument("--k", type=int, default=None)
-    ap.add_argument("--tile-w", type=int, default=16384)
+    ap.add_argument("--tile-w", type=int, default=None,
+                    help="target tile width (default: the engine's choice by shape)")
     ap.add_argument("--denominator", default="rowsum", choices=["rowsum", "diag"])
     ap.add_argument("--venue-skip", type=int, default=None,
                     help="1/0: force venue skipping on/off (default: the engine's)")
@@ -95,6 +96,7 @@ def main():
 
     eng = PathSimEngine(typed, device=dev, tile_w=args.tile_w,
                         denominator=args.denominator)
+    args.tile_w = eng.tile_w
     if args.venue_skip is not None:
         eng.venue_skip = bool(args.venue_skip) and args.denominator == "rowsum"
     eng.upload()

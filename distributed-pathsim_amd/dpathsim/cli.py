@@ -41,7 +41,8 @@ def parse(argv=None):
     ap.add_argument("--topk", type=int, default=10)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--denominator", default="rowsum", choices=["rowsum", "diag"])
-    ap.add_argument("--tile-w", type=int, default=8192)
+    ap.add_argument("--tile-w", type=int, default=None,
+                    help="target tile width (default: the engine's choice by shape)")
     ap.add_argument("--out", help="log path (default: output/d_pathsim_output_<gmtime>.log)")
     ap.add_argument("--shard-dir", help="all-pairs: write per-rank shard files here instead "
                                         "of gathering to rank 0")

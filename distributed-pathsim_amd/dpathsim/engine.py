@@ -18,9 +18,14 @@ import torch
 from . import _lib
 from .graph import TypedTables
 
-# one tile of 16384 targets per wave: 4-bit counters in 8 KiB of LDS (tiles
-# whose bound exceeds 15 take wider passes); 8192 = u8 counters
-DEFAULT_TILE_W = 16384
+# one tile of 16384 targets per wave: 4-bit counters in 8 KiB of LDS (a tile
+# whose bound exceeds 15 runs as two u8 halves); 8192 = u8 counters.  None =
+# by shape (auto_tile_w): the 4-bit tiles pay when a typical row's bound
+# sum_v C[x,v] fits 4 bits -- config3: 7.5 per author, 80.3 -> 75.3 ms per
+# step; config4 (APTPA, ~30 topic papers per author): 224.9 ms at 16384
+# against 205.3 at 8192 (profiles/r03/c45)
+DEFAULT_TILE_W = None
+AUTO_TILE_W_MAX_ROW_SUM = 15.0
 DEFAULT_SPLIT_ROWS = 256    # heaviest rows of a launch cut into pieces
 DEFAULT_PIECES = 16         # target-tile ranges per split row
 DEFAULT_HEAVY_VENUES = 32   # venue skipping: heavy venues in the dense table (64-byte rows)
@@ -78,7 +83,7 @@ class PathSimEngine:
     top-k kernel adds in the score's denominator.
     """
 
-    def __init__(self, typed: TypedTables, device=None, tile_w: int = DEFAULT_TILE_W,
+    def __init__(self, typed: TypedTables, device=None, tile_w: int | None = DEFAULT_TILE_W,
                  denominator: str = "rowsum"):
         if not torch.cuda.is_available():
             raise RuntimeError("PathSimEngine needs a ROCm GPU (torch.cuda.is_available() is False);"
@@ -86,6 +91,10 @@ class PathSimEngine:
         _lib.load()
         self.typed = typed
         self.device = torch.device(device if device is not None else "cuda")
+        self.bounds = None
+        if tile_w is None:
+            self.bounds = host_bounds(typed)
+            tile_w = auto_tile_w(typed, self.bounds)
         if tile_w & (tile_w - 1) or not 256 <= tile_w <= 65536:
             raise ValueError("tile_w must be a power of two in [256, 65536]")
         if denominator not in DENOMINATORS:
@@ -113,7 +122,6 @@ class PathSimEngine:
         self.split_rows = DEFAULT_SPLIT_ROWS
         self.pieces = DEFAULT_PIECES
         self.info = BuildInfo()
-        self.bounds = None
         self.built = False
         self.checked = False
         self._dev = {}
@@ -146,7 +154,8 @@ class PathSimEngine:
                 node_rowid=to(t.node_rowid if g.n_nodes else np.zeros(1, np.int32)),
                 node_colid=to(t.node_colid if g.n_nodes else np.zeros(1, np.int32)),
             )
-        self.bounds = host_bounds(t)
+        if self.bounds is None:
+            self.bounds = host_bounds(t)
         return self
 
     # ------------------------------------------------------------------ build
@@ -636,6 +645,14 @@ def host_bounds(typed: TypedTables) -> Bounds:
     return Bounds(expand=max(expand, 1), sum_c=max(sum_c, 1), key_bits=min(64, gb.bit_length()),
                   max_row_expand=max(int(row_all.max()), 1),
                   max_mids_per_paper=int(pxdeg.max()) if NP else 0)
+
+
+def auto_tile_w(typed: TypedTables, bounds: Bounds) -> int:
+    """Tile width by shape: 16384 (4-bit counters) when the mean over authors of
+    sum_v C[x,v] -- bounded above by the raw expansion count, Bounds.expand --
+    is at most AUTO_TILE_W_MAX_ROW_SUM, else 8192 (u8)."""
+    na = max(typed.n_authors, 1)
+    return 16384 if bounds.expand / na <= AUTO_TILE_W_MAX_ROW_SUM else 8192
 
 
 def build_engine(typed: TypedTables, device=None, tile_w=DEFAULT_TILE_W, timed=False,

@@ -59,11 +59,11 @@ def _topk_rows(eng, k, rows):
 
 def test_config3_all_rows_bench_shape():
     import pathsim_oracle as po
-    from dpathsim.engine import DEFAULT_TILE_W, build_engine
+    from dpathsim.engine import build_engine
     from dpathsim.synth import synth_config
     t = synth_config("config3").typed()
     eng = build_engine(t)                           # the bench configuration
-    assert eng.tile_w == DEFAULT_TILE_W == 16384
+    assert eng.tile_w == 16384 and eng.venue_skip
     got = [a.cpu().numpy() for a in eng.topk(10)]
     t0 = time.perf_counter()
     co = po.COracle.from_typed(t)
