@@ -293,6 +293,7 @@ __device__ __forceinline__ float hv_ratio(uint32_t hv) { return __uint_as_float(
 // of the symmetric mode, the row and the first tile whose pairs it hands on.
 struct RowAux {
   uint32_t ver = 0, cand = 0, ins = 0;
+  uint32_t u8h = 0, wide = 0;   // profiling build: half-tile and wide passes
   int x = 0;               // source row (ordinal)
   int far = INT_MAX;       // sym = 2: targets in tiles >= far may go to records
 };
@@ -917,6 +918,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
             const bool last = X.S.pass + 1 == npass;
             Stage S = X.S;
             const bool u8S = F == 1 || X.u8h;   // this stage's counters: u8 format
+            const bool S_u8h = X.u8h;
             const uint64_t hmS = hm;   // this stage's H (the update below is for the next)
             if (prof) ts[2] = __builtin_amdgcn_s_memtime();
             if (last) {
@@ -972,6 +974,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
               for (int i = 0; i < 4; ++i) pc[i] += ts[i + 1] - ts[i];
               ++pc[4];
               if (last) { pc[5] += ts[5] - ts[2]; pc[6] += ts[6] - ts[5]; }
+              ra.u8h += S_u8h ? 1u : 0u;            // passes over a u8 half tile
+              ra.wide += S.lnp > 0 ? 1u : 0u;       // passes with wider counters
             }
             if (last) break;
           }
@@ -1028,6 +1032,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
     for (int i = 0; i < 7; ++i) atomicAdd(p.counter + 8 + i, static_cast<unsigned long long>(pc[i]));
     atomicAdd(p.counter + 15, static_cast<unsigned long long>(ra.cand));
     atomicAdd(p.counter + 16, static_cast<unsigned long long>(ra.ins));
+    atomicAdd(p.counter + 17, static_cast<unsigned long long>(ra.u8h));
+    atomicAdd(p.counter + 18, static_cast<unsigned long long>(ra.wide));
   }
 }
 

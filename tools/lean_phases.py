@@ -22,5 +22,7 @@ tot = sum(c[8:12])
 print(f"  prefetch split: refilter+stage_make {c[13] / st:.0f}, issue batch 0 {c[14] / st:.0f}, rest {(c[10] - c[13] - c[14]) / st:.0f}", flush=True)
 print(f"candidates scored {c[15]} ({c[15] / st:.1f} per stage, {c[15] / R:.1f} per row), "
       f"inserted {c[16]} ({c[16] / R:.1f} per row)", flush=True)
+print(f"passes over u8 half tiles {c[17]} ({c[17] / st:.3f} of stages), with wider counters "
+      f"{c[18]} ({c[18] / st:.4f})", flush=True)
 print(f"stages {st} ({st / R:.1f} per row); cycles per wave-stage: " +
       " ".join(f"{n} {c[8 + i] / st:.0f} ({c[8 + i] / tot:.0%})" for i, n in enumerate(names)), flush=True)
