@@ -76,8 +76,16 @@ template <> struct Fmt<2> {
   static constexpr int BITS = 4;
   static constexpr uint32_t UB0 = 0xFu;
 };
+// Knobs, swept on the full config3 launch at W = 16384 (profiles/r03/ab7-ab9):
+// epilogue blocks per trip 1 / 2 = 72.3 / 73.2 ms; boundary selects before the
+// counting path 4 / 8 / 16 = 72.3 / 73.2 / 73.8 ms; flush the candidate queue
+// once the list is full at 8 / 12 / 16 / 24 / 32 / 48 candidates (earlier
+// flushes raise tau sooner) -- together 69.3-70.0 against 73.1 ms.
 #ifndef DPS_EPI1
-#define DPS_EPI1 2
+#define DPS_EPI1 1
+#endif
+#ifndef DPS_FLUSH_AT
+#define DPS_FLUSH_AT 12   // queued candidates that trigger a flush once the list is full
 #endif
 constexpr int kEpi1 = DPS_EPI1;                // epilogue blocks read per trip
 
@@ -639,7 +647,10 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
 // up to kSel of them by a per-boundary select over readlane'd scalars, more by
 // counting the boundaries each lane has passed and fetching base and C from
 // that venue's lane with two independent bpermutes.
-constexpr int kSel = 8;
+#ifndef DPS_KSEL
+#define DPS_KSEL 4
+#endif
+constexpr int kSel = DPS_KSEL;
 
 __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __restrict__ ent,
                                        int lane, Batch& B) {
@@ -884,7 +895,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
             if (prof) ts[1] = __builtin_amdgcn_s_memtime();
             // score what is queued while the list is filling or the queue is
             // half full (one memory round trip per 64 candidates)
-            if (Q.n > 0 && (!top.full() || Q.n >= kWave / 2))
+            if (Q.n > 0 && (!top.full() || Q.n >= DPS_FLUSH_AT))
               vq_flush<KPL, HV, SY>(p, Q, top, Q.n < kWave ? Q.n : kWave, gx, lane, c, hv, hm, ra);
             const double tau = top.full() ? top.kth_s : -1.0;
             int mseg = 1;
