@@ -25,7 +25,12 @@ for W, NW in cases:
     if W != W0:
         eng = None
         torch.cuda.empty_cache()
-        eng, W0 = build_engine(t, tile_w=W), W
+        from dpathsim.engine import PathSimEngine
+        eng = PathSimEngine(t, tile_w=W)
+        if os.environ.get("AB_NHEAVY"):
+            eng.n_heavy = int(os.environ["AB_NHEAVY"])
+        eng.upload().build()
+        W0 = W
         eng.build(timed=True)
         ph = eng.info.phase_ms
         print("  build ms: " + " ".join(f"{k} {v:.3f}" for k, v in ph.items() if k != "host_total")

@@ -17,3 +17,8 @@ for run in ${AB_RUNS:-cur:}; do
     || { echo "ab $n failed"; tail -30 $O/ab_$n.log; exit 1; }
   echo "$n:"; grep -v amdgpu.ids $O/ab_$n.log
 done
+# heavy-venue table sizes (venue skipping) with the in-tree library
+for nh in ${AB_NHEAVY_LIST:-}; do
+  AB_NHEAVY=$nh timeout -k 10 300 python -u tools/ab_w.py > $O/ab_nheavy$nh.log 2>&1 || { echo "ab nheavy $nh failed"; tail -30 $O/ab_nheavy$nh.log; exit 1; }
+  echo "n_heavy $nh:"; grep -v amdgpu.ids $O/ab_nheavy$nh.log
+done
