@@ -1,0 +1,19 @@
+#!/bin/bash
+# Configs 4 and 5 with the engine's own defaults (tile width and venue
+# skipping chosen by the engine), bench.py, 3 steps each.
+set -u
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-r03cfg}
+mkdir -p $O
+for c in ${CONFIGS:-config4 config5}; do
+  timeout -k 10 400 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_$c.log 2>&1 \
+    || { echo "bench $c failed"; tail -20 $O/bench_$c.log; exit 1; }
+  python3 - <<PY
+import json
+r = json.loads([l for l in open("$O/bench_$c.log") if l.startswith("{")][-1])
+rf = r["roofline"]
+print("$c", "tile_w", r["config"]["tile_w"], "venue_skip", rf.get("venue_skip"), "ms/step %.1f" % r["ms_per_step"],
+      "cct %.1f" % r["phases_ms"]["cct_topk"], "value %.3e" % r["value"], "frac %.3f" % rf["frac"], flush=True)
+PY
+done
