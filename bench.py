@@ -65,8 +65,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dpathsim.dist import (RcclComm, balanced_bounds, balanced_edges, gather_topk_compact,
-                               max_shard, pack_counts)
+    from dpathsim.dist import RcclComm, gather_topk_compact, max_shard, pack_counts, shard_edges
     from dpathsim.engine import PathSimEngine
     from dpathsim.synth import CONFIGS, synth_config
 
@@ -77,16 +76,21 @@ def main():
     # driver): all ranks on one device, the gather over gloo instead of RCCL
     local = int(os.environ.get("DPATHSIM_BENCH_DEVICE", local))
     backend = os.environ.get("DPATHSIM_BENCH_BACKEND", "rccl")
+    # the top-k gather over RCCL (xGMI): torch.distributed's "nccl" process group
+    # by default; DPATHSIM_BENCH_COMM=capi runs it through libdpathsim's C ABI
+    # (dps_comm_init / dps_gather, gloo as the control plane) instead -- that
+    # path has only run with one rank so far, so it is opt-in
+    comm_kind = os.environ.get("DPATHSIM_BENCH_COMM", "torch")
     comm = None
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
-        # gloo carries the control plane only (RCCL unique id, barriers, the
-        # max over ranks of the step time); the top-k gather is RCCL over xGMI
-        # through libdpathsim's C ABI (dps_comm_init / dps_gather)
-        dist.init_process_group("gloo")
-        if backend == "rccl":
-            comm = RcclComm(device=dev)
+        if backend == "rccl" and comm_kind == "torch":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+            if backend == "rccl":
+                comm = RcclComm(device=dev)
 
     na_cfg, np_cfg, nm_cfg, mp_name, k_cfg = CONFIGS[args.config]
     k = args.k or k_cfg
@@ -101,33 +105,37 @@ def main():
         eng.venue_skip = bool(args.venue_skip) and args.denominator == "rowsum"
     eng.upload()
 
-    def plan():
-        # contiguous row shards of equal estimated work (every rank derives the
-        # same bounds from its own, identical C: no communication)
-        return balanced_bounds(eng.row_work(), world) if world > 1 else [(0, NA)]
-
     eng.build()             # checks the overflow conditions once (one sync)
-    bounds0 = plan()
+    # contiguous row shards of equal estimated work (dps_shard_edges over the
+    # build's row work; every rank derives the same edges from its own,
+    # identical C: no communication), read back once, outside the timed loop
+    edges0 = shard_edges(eng.tensor("row_terms")[:NA], world)
+    e_host = edges0.cpu().tolist()
+    bounds0 = [(e_host[r], e_host[r + 1]) for r in range(world)]
     m = max_shard(NA, world, bounds0)
     out = (torch.empty((m, k), dtype=torch.int32, device=dev),
            torch.empty((m, k), dtype=torch.int64, device=dev),
            torch.empty((m, k), dtype=torch.float64, device=dev))
     packed = torch.empty((m, k), dtype=torch.int64, device=dev)
-    gathered = None
+    gathered = final = None
     if world > 1 and rank == 0:
         gathered = torch.empty((world * m, k), dtype=torch.int64, device=dev)
+        final = (torch.empty((NA, k), dtype=torch.int32, device=dev),
+                 torch.empty((NA, k), dtype=torch.int64, device=dev),
+                 torch.empty((NA, k), dtype=torch.float64, device=dev))
 
     ev_topk = []
     # every step re-derives the shards from its own C on the device (no host
     # read-back inside the step); the launch uses the shards of the first build
     # and any difference is raised after the timed loop
-    edges0 = torch.tensor([a for a, _ in bounds0] + [NA], dtype=torch.int64, device=dev)
+    edges_step = torch.empty_like(edges0)
     plan_mismatch = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def step(record):
         eng.build(check=False)   # no host read-back inside the step; checked after timing
         if world > 1:
-            plan_mismatch.add_((balanced_edges(eng.row_work(), world) != edges0).sum())
+            shard_edges(eng.tensor("row_terms")[:NA], world, out=edges_step, ref=edges0,
+                        mismatch=plan_mismatch)
         r0, r1 = bounds0[rank]
         bounds = bounds0
         view = tuple(t[:r1 - r0] for t in out)
@@ -140,11 +148,12 @@ def main():
             e1.record()
             ev_topk.append((e0, e1))
         if world > 1:   # one packed buffer per rank, gathered to rank 0 (RCCL)
-            # 8 B per slot on the wire: (count << 32) | index; rank 0 rebuilds
-            # the fp64 scores from its own g (the same exact division)
+            # 8 B per slot on the wire: (count << 32) | index (dps_pack_counts);
+            # rank 0 puts the rows in order and rebuilds the fp64 scores from its
+            # own g with the same exact division (dps_unpack_gathered)
             pack_counts(out[0], out[1], out=packed)
             gather_topk_compact(packed, eng.tensor("den")[:NA], NA, world, out=gathered,
-                                bounds=bounds, comm=comm)
+                                bounds=bounds, comm=comm, edges=edges0, result=final)
 
     for _ in range(args.warmup):
         step(False)
@@ -164,7 +173,8 @@ def main():
     if int(plan_mismatch.item()) != 0:
         raise RuntimeError("row shards changed between steps")
     if world > 1:
-        te = torch.tensor([elapsed], dtype=torch.float64)
+        te = torch.tensor([elapsed], dtype=torch.float64,
+                          device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         elapsed = float(te.item())
     ms_per_step = elapsed * 1e3 / args.steps

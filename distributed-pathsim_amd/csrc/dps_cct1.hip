@@ -112,27 +112,42 @@ __device__ __forceinline__ float wave_min_f32(float v) {
 struct Win1 {
   int w0;          // first tile of the window (wave-uniform)
   uint32_t ub;     // lane: UB of the tile (0xFFFFFFFF = unbounded)
+  uint32_t hb;     // dual (F = 2 with companion u8 tiles): the bounds of the
+                   // tile's two u8 halves 2t, 2t+1, 16 bits each (kHalfSat =
+                   // 65535 or more: the half takes the tile's own bound)
   float gmf;       // lane: smallest g of the tile, as float
   uint64_t live;   // tiles not yet visited that may hold a top-k target
   uint64_t ykeep;  // symmetric rest pass: tiles that may hold a pair to hand on
   double tau;      // tau the mask was last filtered with
 };
+constexpr uint32_t kHalfSat = 0xFFFFu;
 
 // UB of tiles w0 + lane over all d venues of the row (lane j of c / vT holds
-// venue j of the first 64; rows with more venues reload them per group).
+// venue j of the first 64; rows with more venues reload them per group) and,
+// when dual, the bounds of the tile's two companion u8 halves in the same
+// loop (hb, see Win1): computed here lane-parallel, once per window, instead
+// of one wave reduction with an exposed h_maxc load per split tile in the
+// stage transition (round 4; the load's vmcnt wait also drained the next
+// stage's just-issued chunk loads).
 __device__ __forceinline__ uint32_t win_ub(const CctParams& p, int w0, int t_end, int64_t pb, int d,
-                                           int c, uint32_t vT, int lane) {
+                                           int c, uint32_t vT, uint32_t vT8, bool dual, int lane,
+                                           uint32_t& hb) {
   const int t = w0 + lane;
   const bool in = t < t_end;
+  hb = kHalfSat | (kHalfSat << 16);
   if (!p.use_bounds) return 0xFFFFFFFFu;        // no tile bounds: every tile, 32-bit passes
-  uint64_t acc = 0;
+  uint64_t acc = 0, ha = 0, hz = 0;
+  const bool in_a = dual && in;                  // half 2t always exists when t does
+  const bool in_b = dual && in && 2 * t + 1 < p.T8;
   for (int g0 = 0; g0 < d; g0 += kWave) {
     int cg = c;
-    uint32_t vg = vT;
+    uint32_t vg = vT, vg8 = vT8;
     if (g0 > 0) {
       const int j = g0 + lane;
       cg = j < d ? p.c_val[pb + j] : 0;
-      vg = j < d ? static_cast<uint32_t>(p.c_col[pb + j]) * static_cast<uint32_t>(p.T) : 0u;
+      const uint32_t vj = j < d ? static_cast<uint32_t>(p.c_col[pb + j]) : 0u;
+      vg = vj * static_cast<uint32_t>(p.T);
+      vg8 = dual ? vj * static_cast<uint32_t>(p.T8) : 0u;
     }
     const int nj = d - g0 < kWave ? d - g0 : kWave;
 #pragma unroll 4
@@ -141,7 +156,19 @@ __device__ __forceinline__ uint32_t win_ub(const CctParams& p, int w0, int t_end
       const uint32_t vj = readlane(vg, j);
       const uint32_t mx = in ? p.tile_maxc[vj + static_cast<uint32_t>(t)] : 0u;
       acc += static_cast<uint64_t>(cj) * mx;
+      if (dual) {
+        const uint32_t vj8 = readlane(vg8, j) + 2u * static_cast<uint32_t>(t);
+        const uint32_t ma = in_a ? p.h_maxc[vj8] : 0u;
+        const uint32_t mb = in_b ? p.h_maxc[vj8 + 1u] : 0u;
+        ha += static_cast<uint64_t>(cj) * ma;
+        hz += static_cast<uint64_t>(cj) * mb;
+      }
     }
+  }
+  if (dual) {
+    const uint32_t a = ha >= kHalfSat ? kHalfSat : static_cast<uint32_t>(ha);
+    const uint32_t b = hz >= kHalfSat ? kHalfSat : static_cast<uint32_t>(hz);
+    hb = a | (b << 16);
   }
   return acc >= 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(acc);
 }
@@ -155,12 +182,12 @@ __device__ __forceinline__ uint64_t win_pass(const Win1& w, double tau, float gx
 
 template <bool SY>
 __device__ __forceinline__ void win_load(const CctParams& p, Win1& w, int w0, int t_lo, int t_end,
-                                         int64_t pb, int d, int c, uint32_t vT, int lane,
-                                         double tau, float gxf, int far) {
+                                         int64_t pb, int d, int c, uint32_t vT, uint32_t vT8,
+                                         bool dual, int lane, double tau, float gxf, int far) {
   w.w0 = w0;
   const int t = w0 + lane;
   w.gmf = t < t_end ? i64_f32(p.tile_gmin[t]) : 0.0f;
-  w.ub = win_ub(p, w0, t_end, pb, d, c, vT, lane);
+  w.ub = win_ub(p, w0, t_end, pb, d, c, vT, vT8, dual, lane, w.hb);
   w.ykeep = 0;
   if (SY && far != INT_MAX) {
     // a far tile stays while its bound reaches the smallest count any of its
@@ -176,17 +203,20 @@ __device__ __forceinline__ void win_load(const CctParams& p, Win1& w, int w0, in
 // Next tile to process (-1: none left); slides the window as needed.
 template <bool SY>
 __device__ __forceinline__ int next_tile(const CctParams& p, Win1& w, int t_end, int64_t pb, int d,
-                                         int c, uint32_t vT, int lane, double tau, float gxf,
-                                         uint32_t& ub_t, int far) {
+                                         int c, uint32_t vT, uint32_t vT8, bool dual, int lane,
+                                         double tau, float gxf, uint32_t& ub_t, uint32_t& hb_t,
+                                         int far) {
   for (;;) {
     if (w.live) {
       const int b = __builtin_ctzll(w.live);
       w.live &= w.live - 1;
       ub_t = readlane(w.ub, b);
+      if (dual) hb_t = readlane(w.hb, b);
       return w.w0 + b;
     }
     if (w.w0 + kWave >= t_end) return -1;
-    win_load<SY>(p, w, w.w0 + kWave, w.w0 + kWave, t_end, pb, d, c, vT, lane, tau, gxf, far);
+    win_load<SY>(p, w, w.w0 + kWave, w.w0 + kWave, t_end, pb, d, c, vT, vT8, dual, lane, tau, gxf,
+                 far);
   }
 }
 
@@ -814,14 +844,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       Win1 w;
       int h_next = -1;            // the second half of a split wide tile, pending
       uint32_t h_ub = 0;
-      // bound of u8 half t8 over the row's venues (wave sum of C[x,v] * maxc;
-      // rows with more than 64 venues, or a product beyond 16 bits, keep ub4)
-      auto half_ub = [&](int t8, uint32_t ub4) -> uint32_t {
-        if (!p.use_bounds || d > kWave) return ub4;
-        const uint32_t mx = lane < d0 ? p.h_maxc[vT8 + static_cast<uint32_t>(t8)] : 0u;
-        const uint32_t pr = static_cast<uint32_t>(c) * mx;
-        if (ballot(mx > 0xFFFFu || pr > 0xFFFFu)) return ub4;
-        return wave_sum_u32(pr);
+      // bound of a u8 half from the window (kHalfSat: 65535 or more -> the
+      // 4-bit tile's own bound ub4, which also covers the half)
+      auto half_ub = [&](uint32_t h, uint32_t ub4) -> uint32_t {
+        return h >= kHalfSat ? ub4 : h;
       };
       // next stage: the pending half, else the next live tile -- split into its
       // two u8 halves when dual and its 4-bit bound exceeds 15
@@ -834,11 +860,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
           h_next = -1;
           return;
         }
-        tn = next_tile<SY>(p, w, t_end, pb, d, c, vT, lane, tau, gxf, ubn, ra.far);
+        uint32_t hbn = 0;
+        tn = next_tile<SY>(p, w, t_end, pb, d, c, vT, vT8, dual, lane, tau, gxf, ubn, hbn, ra.far);
         if (!dual || tn < 0 || ubn <= Fmt<F>::UB0) return;
         const int ta = 2 * tn, tb = 2 * tn + 1;
-        const uint32_t ua = half_ub(ta, ubn);
-        const uint32_t ubb = tb < p.T8 ? half_ub(tb, ubn) : 0u;
+        const uint32_t ua = half_ub(hbn & 0xFFFFu, ubn);
+        const uint32_t ubb = tb < p.T8 ? half_ub(hbn >> 16, ubn) : 0u;
         u8n = true;
         if (ua == 0) {            // only the second half holds this row's entries
           tn = tb;
@@ -859,7 +886,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
           hv = hv_pack(static_cast<float>(static_cast<double>(c) / static_cast<double>(p.s[v])) *
                            (1.0f + 0x1p-20f), sl);
       }
-      win_load<SY>(p, w, t_beg, t_beg, t_end, pb, d, c, vT, lane, -1.0, gxf, ra.far);
+      win_load<SY>(p, w, t_beg, t_beg, t_end, pb, d, c, vT, vT8, dual, lane, -1.0, gxf, ra.far);
       uint32_t ub_t = 0;
       int t0;
       bool u8n;

@@ -100,6 +100,10 @@ SIGNATURES = {
     "dps_bcast": (C.c_int, [_p, _p, _sz, _i32, _p]),
     "dps_gather": (C.c_int, [_p, _p, _p, _sz, _i32, _p]),
     "dps_get_tuning": (C.c_int, [_i32]),
+    "dps_shard_edges_workspace_size": (_sz, [_i64]),
+    "dps_shard_edges": (C.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
+    "dps_pack_counts": (C.c_int, [_p, _p, _i64, _p, _p]),
+    "dps_unpack_gathered": (C.c_int, [_p, _i32, _i64, _i32, _p, _i64, _p, _p, _p, _p, _p]),
     "dps_topk_merge": (C.c_int, [_p, _p, _p, _p, _i64, _i32, _i32, _i64, _i64, _p, _p, _p, _p]),
     "dps_heavy_first_workspace_size": (_sz, [_i64]),
     "dps_heavy_first": (C.c_int, [_p, _i64, _i64, _i64, _i32, _p, _p, _sz, _p]),

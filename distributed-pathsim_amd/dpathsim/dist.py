@@ -48,7 +48,9 @@ class RcclComm:
         cpu = dist.get_backend(group) != "nccl"
         t = torch.tensor(bytearray(buf), dtype=torch.uint8,
                          device="cpu" if cpu else self.device)
-        dist.broadcast(t, src=0, group=group)
+        # src is a GLOBAL rank: the group's rank 0 (a subgroup need not hold rank 0)
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast(t, src=src, group=group)
         buf = (C.c_uint8 * nb)(*t.cpu().tolist())
         h = C.c_void_p()
         with torch.cuda.device(self.device):
@@ -119,6 +121,48 @@ def balanced_edges(work: torch.Tensor, world: int) -> torch.Tensor:
     return torch.cummax(edges, 0).values
 
 
+def _stream(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def shard_edges(terms: torch.Tensor, world: int, out: torch.Tensor | None = None,
+                ref: torch.Tensor | None = None, mismatch: torch.Tensor | None = None):
+    """Shard edges from the build's per-row work terms (``row_terms``): the same
+    plan as ``balanced_edges(terms + (terms.sum() // n) // 2, world)``
+    (PathSimEngine.row_work), computed by dps_shard_edges on the device for a
+    device tensor -- one scan and a binary search per cut, nothing read back,
+    no PyTorch compute.  ``ref`` / ``mismatch``: add the number of edges that
+    differ from ``ref`` to the int64 device scalar ``mismatch`` (the timed
+    step's plan check).  Host tensors (the CPU gloo tests) take the same
+    arithmetic in PyTorch."""
+    n = int(terms.numel())
+    if not terms.is_cuda:
+        w = terms.to(torch.int64)
+        hm = (w.sum() // max(n, 1)) // 2 if n else 0
+        e = balanced_edges(w + hm, world) if world > 1 and n else \
+            torch.tensor([shard_bounds(n, r, world)[0] for r in range(world)] + [n], dtype=torch.int64)
+        if out is not None:
+            out.copy_(e)
+        if ref is not None:
+            mismatch.add_((e != ref.to(e.device)).sum().to(mismatch.device))
+        return e if out is None else out
+    from . import _lib
+    terms = terms.contiguous()
+    if terms.dtype != torch.int64:
+        raise TypeError("terms must be int64")
+    if out is None:
+        out = torch.empty(world + 1, dtype=torch.int64, device=terms.device)
+    if ref is not None and mismatch is None:
+        raise ValueError("ref needs a mismatch counter")
+    ws = torch.empty(max(_lib.size("dps_shard_edges_workspace_size", n), 256), dtype=torch.uint8,
+                     device=terms.device)
+    _lib.call("dps_shard_edges", terms.data_ptr(), n, world, out.data_ptr(),
+              ref.data_ptr() if ref is not None else None,
+              mismatch.data_ptr() if mismatch is not None else None, ws.data_ptr(), ws.numel(),
+              _stream(terms))
+    return out
+
+
 def balanced_bounds(work: torch.Tensor, world: int) -> list[tuple[int, int]]:
     """Contiguous shards of (nearly) equal total work.
 
@@ -176,7 +220,7 @@ def gather_topk(parts, n_rows: int, world: int, group=None, out=None, bounds=Non
     src = packed.contiguous() if nccl else packed.contiguous().cpu()
     recv = None
     if rank == dst:
-        if out is None or not nccl:
+        if not nccl or not _recv_ok(out, world * m, int(packed.shape[1]), src.device):
             out = torch.empty((world * m, packed.shape[1]), dtype=torch.int64,
                               device=src.device)
         recv = list(out.view(world, m, packed.shape[1]).unbind(0))
@@ -193,18 +237,70 @@ def gather_topk(parts, n_rows: int, world: int, group=None, out=None, bounds=Non
 # ------------------------------------------------------ compact (8 B) gather
 def pack_counts(idx: torch.Tensor, cnt: torch.Tensor, out=None):
     """(idx int32, cnt int64) [R, k] -> int64 [R, k] = (count << 32) | index: the
-    score is NOT sent -- the root recomputes it (:func:`rescore`)."""
+    score is NOT sent -- the root recomputes it (:func:`rescore`).  Device
+    tensors: dps_pack_counts (HIP); host tensors: the same in PyTorch."""
     if out is None:
         out = torch.empty(idx.shape, dtype=torch.int64, device=idx.device)
+    if idx.is_cuda:
+        from . import _lib
+        if not (idx.is_contiguous() and cnt.is_contiguous() and out.is_contiguous()
+                and idx.dtype == torch.int32 and cnt.dtype == torch.int64
+                and out.dtype == torch.int64 and idx.shape == cnt.shape
+                and out.numel() >= idx.numel()):
+            raise ValueError("pack_counts: contiguous int32 idx / int64 cnt / int64 out of one shape")
+        _lib.call("dps_pack_counts", idx.data_ptr(), cnt.data_ptr(), idx.numel(), out.data_ptr(),
+                  _stream(idx))
+        return out
     torch.bitwise_or(cnt.to(torch.int64) << 32, idx.to(torch.int64) & 0xFFFFFFFF, out=out)
     return out
+
+
+def unpack_gathered(gathered: torch.Tensor, world: int, m: int, edges: torch.Tensor,
+                    den: torch.Tensor, out=None):
+    """Rank 0's gathered [world * m, k] words -> (idx, cnt, score) of rows
+    [edges[0], edges[world]) in row order (dps_unpack_gathered, HIP): rank r's
+    rows are gathered rows r*m ..; the score is the kernel's division of the
+    same exact integers, bit-identical.  ``edges``: int64 device [world + 1];
+    its host copy gives the row count (pass ``out`` to skip that read)."""
+    from . import _lib
+    k = int(gathered.shape[1])
+    if out is None:
+        e = edges.cpu()
+        n = int(e[world] - e[0])
+        out = (torch.empty((n, k), dtype=torch.int32, device=gathered.device),
+               torch.empty((n, k), dtype=torch.int64, device=gathered.device),
+               torch.empty((n, k), dtype=torch.float64, device=gathered.device))
+    idx, cnt, sc = out
+    n = int(idx.shape[0])
+    for t, dt in ((idx, torch.int32), (cnt, torch.int64), (sc, torch.float64)):
+        if not (t.is_contiguous() and t.dtype == dt and tuple(t.shape) == (n, k)
+                and t.device == gathered.device):
+            raise ValueError("unpack_gathered: outputs must be contiguous [n, k] int32 / int64 / f64 "
+                             "on the gathered tensor's device")
+    if not (gathered.is_contiguous() and gathered.dtype == torch.int64 and edges.is_cuda
+            and edges.dtype == torch.int64 and edges.numel() == world + 1
+            and gathered.shape[0] >= world * m):
+        raise ValueError("unpack_gathered: int64 gathered [>= world*m, k] and int64 device edges [world+1]")
+    den = den.contiguous()
+    _lib.call("dps_unpack_gathered", gathered.data_ptr(), world, m, k, edges.data_ptr(), n,
+              den.data_ptr(), idx.data_ptr(), cnt.data_ptr(), sc.data_ptr(), _stream(gathered))
+    return idx, cnt, sc
 
 
 def rescore(packed: torch.Tensor, den: torch.Tensor, row_begin: int = 0):
     """(idx, cnt, score) from :func:`pack_counts` words of rows row_begin...:
     score = double(2 cnt) / double(den[x] + den[y]) -- the hot kernel's one fp64
     division of the same exact integers (DPathSim_APVPA.py:51-52), so the bits
-    are identical -- and 0.0 for zero counts and empty (-1) slots."""
+    are identical -- and 0.0 for zero counts and empty (-1) slots.  Device
+    tensors: dps_unpack_gathered (HIP); host tensors: the same in PyTorch."""
+    if packed.is_cuda:
+        R = int(packed.shape[0])
+        edges = torch.tensor([row_begin, row_begin + R], dtype=torch.int64, device=packed.device)
+        k = int(packed.shape[1])
+        out = (torch.empty((R, k), dtype=torch.int32, device=packed.device),
+               torch.empty((R, k), dtype=torch.int64, device=packed.device),
+               torch.empty((R, k), dtype=torch.float64, device=packed.device))
+        return unpack_gathered(packed.contiguous(), 1, R, edges, den.to(packed.device), out=out)
     idx = (packed & 0xFFFFFFFF).to(torch.int32)
     cnt = packed >> 32
     rows = torch.arange(row_begin, row_begin + packed.shape[0], device=packed.device)
@@ -216,16 +312,28 @@ def rescore(packed: torch.Tensor, den: torch.Tensor, row_begin: int = 0):
     return idx, cnt, score
 
 
+def _recv_ok(out, rows, cols, device) -> bool:
+    """A caller-supplied receive buffer is used only if it is exactly what the
+    collective writes: contiguous int64 [rows, cols] on ``device``."""
+    return (out is not None and out.is_contiguous() and out.dtype == torch.int64
+            and tuple(out.shape) == (rows, cols) and out.device == device)
+
+
 def gather_topk_compact(parts, den: torch.Tensor, n_rows: int, world: int, group=None,
                         out=None, bounds=None, dst: int = 0, force_collective: bool = False,
-                        comm: RcclComm | None = None):
+                        comm: RcclComm | None = None, edges: torch.Tensor | None = None,
+                        result=None):
     """As :func:`gather_topk`, with 8 B per slot on the wire: every rank sends
     (count << 32) | index words; rank ``dst`` rebuilds the scores from its own
     copy of the denominator term ``den`` (every rank holds all of g).  ``parts``:
     (idx, cnt[, score]) [max_shard, k] or packed int64 [max_shard, k].
     ``comm``: gather with libdpathsim's RCCL communicator (dps_gather) instead
     of torch.distributed.  ``force_collective`` runs the gather even for one
-    rank (lets a one-GPU box exercise the RCCL call)."""
+    rank (lets a one-GPU box exercise the RCCL call).  On the device the
+    rows are put back in order and rescored by one HIP kernel
+    (dps_unpack_gathered) reading the gathered buffer in place; ``edges`` (int64
+    device [world + 1], the shard edges) and ``result`` ((idx, cnt, score)
+    [n_rows, k]) avoid building them from ``bounds`` inside a timed step."""
     if bounds is None:
         bounds = [shard_bounds(n_rows, r, world) for r in range(world)]
     packed = parts if isinstance(parts, torch.Tensor) else pack_counts(parts[0], parts[1])
@@ -234,27 +342,35 @@ def gather_topk_compact(parts, den: torch.Tensor, n_rows: int, world: int, group
     m = max_shard(n_rows, world, bounds)
     if packed.shape[0] != m:
         raise ValueError(f"part has {packed.shape[0]} rows, expected max_shard {m}")
+    cols = int(packed.shape[1])
+
+    def finish(buf):
+        if buf.is_cuda:
+            e = edges if edges is not None else torch.tensor(
+                [a for a, _ in bounds] + [bounds[-1][1]], dtype=torch.int64, device=buf.device)
+            return unpack_gathered(buf, world, m, e, den.to(buf.device), out=result)
+        full = torch.cat([buf[r * m: r * m + (b - a)] for r, (a, b) in enumerate(bounds)])
+        return rescore(full, den.to(full.device))
+
     if comm is not None:
-        if comm.rank == dst and (out is None or out.numel() < world * m * packed.shape[1]):
-            out = torch.empty((world * m, packed.shape[1]), dtype=torch.int64, device=packed.device)
+        if comm.rank == dst and not _recv_ok(out, world * m, cols, packed.device):
+            out = torch.empty((world * m, cols), dtype=torch.int64, device=packed.device)
         comm.gather(packed, out if comm.rank == dst else None, root=dst)
         if comm.rank != dst:
             return None
-        full = torch.cat([out[r * m: r * m + (b - a)] for r, (a, b) in enumerate(bounds)])
-        return rescore(full, den)
+        return finish(out)
     rank = dist.get_rank(group)
     nccl = dist.get_backend(group) == "nccl"
     src = packed.contiguous() if nccl else packed.contiguous().cpu()
     recv = None
     if rank == dst:
-        if out is None or not nccl:
-            out = torch.empty((world * m, packed.shape[1]), dtype=torch.int64, device=src.device)
-        recv = list(out.view(world, m, packed.shape[1]).unbind(0))
+        if not nccl or not _recv_ok(out, world * m, cols, src.device):
+            out = torch.empty((world * m, cols), dtype=torch.int64, device=src.device)
+        recv = list(out.view(world, m, cols).unbind(0))
     dist.gather(src, gather_list=recv, dst=dst, group=group)
     if rank != dst:
         return None
-    full = torch.cat([out[r * m: r * m + (b - a)] for r, (a, b) in enumerate(bounds)])
-    return rescore(full.to(packed.device), den)
+    return finish(out.to(packed.device))
 
 
 # ------------------------------------------------------- per-rank shard files

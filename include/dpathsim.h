@@ -253,20 +253,32 @@ int dps_target_order(const int64_t* g, int64_t n_targets, int32_t key_bits,
  * A5 operand layout, step 2: target-tiled transpose of C for the C.C^T kernels.
  * Target labels (t_rank[y], or y if t_rank == NULL) in [0, n_targets) are cut
  * into tiles of `tile_w` (power of two, 256..65536; the hot kernel keeps one
- * tile's packed u8 accumulators in LDS).  Bucket (v, t) holds, for every y of
- * tile t with C[y,v] > 0, packed entries in one of two formats:
- *   tile_w <= 8192: uint16 (l << 3) | e, l = label(y) - t*tile_w, one piece
- *                   of value 2^e; C[y,v] is split into power-of-two pieces that
- *                   sum to it (e <= 7, and e <= 5 when l % 4 == 3: e = 6, 7 at
- *                   l % 4 == 3 are padding codes);
- *   tile_w >= 16384: uint32 (C[y,v] << 16) | (label(y) - t*tile_w).
- * Buckets are stored contiguously in [v][t] order: bucket (v,t) is the uint32
- * words tile_ent[tile_off[v*T + t] .. tile_off[v*T + t + 1]),
+ * tile's packed counters in LDS: u8 at tile_w 8192, 4-bit at 16384).  Bucket
+ * (v, t) holds, for every y of tile t with C[y,v] > 0, packed entries in one of
+ * three formats, l = label(y) - t*tile_w:
+ *   tile_w <= 8192:  uint16 (l << 3) | e, one piece of value 2^e: C[y,v] is
+ *                    split into power-of-two pieces that sum to it (as many
+ *                    2^emax as fit, then the set bits of the rest), emax = 7,
+ *                    or 5 when l % 4 == 3 (e = 6, 7 at l % 4 == 3 are padding
+ *                    codes).  The low five bits 8*(l % 4) + e are the shift
+ *                    that adds C[x,v]*2^e to target l's byte of a packed-u8
+ *                    dword;
+ *   tile_w == 16384: uint16 (l << 2) | e, the same for packed 4-bit counters:
+ *                    emax = 3, or 1 when l % 8 == 7 (e = 2, 3 at l % 8 == 7 are
+ *                    padding codes); low five bits 4*(l % 8) + e;
+ *   tile_w >= 32768: uint32 (C[y,v] << 16) | l, one entry per (y, v).
+ * To decode a 16-bit entry h: l = h >> 3 (resp. >> 2), value = 1 << (h & 7)
+ * (resp. & 3), skipping padding codes; summing the values of one (v, l) gives
+ * C[y,v].  16-bit entries are packed two per uint32 word, the first in the low
+ * half.  Buckets are stored contiguously in [v][t] order: bucket (v,t) is the
+ * uint32 words tile_ent[tile_off[v*T + t] .. tile_off[v*T + t + 1]),
  * T = ceil(n_targets/tile_w).  Every bucket is padded to 16 bytes (32-bit:
- * C = 0 entries; 16-bit: groups of padding codes {7,7} / {7,6,6} on one
- * dword, which add C * 2^32 == 0 to packed u8 accumulators), so bucket starts are 16-byte aligned and 16-byte chunks never straddle
- * buckets.  tile_off uint32[n_mids*T + 1] (word offsets), tile_ent
- * uint32[dps_ct_tiles_ent_capacity()].
+ * C = 0 entries; 16-bit: groups of padding codes on one dword -- {7,7} / {7,6,6}
+ * at u8, {3,3} / {3,2,2} at 4-bit, each group at one label of a dword's last
+ * target (l % 4 == 3, resp. l % 8 == 7) -- which add
+ * C * 2^32 == 0 to the packed accumulators), so bucket starts are 16-byte
+ * aligned and 16-byte chunks never straddle buckets.  tile_off
+ * uint32[n_mids*T + 1] (word offsets), tile_ent uint32[dps_ct_tiles_ent_capacity()].
  * Optional: tile_maxc uint32[n_mids*T + 1] = max C[y,v] per bucket;
  * tile_gmin int64[T] = min g[y] per tile (needs g).
  * Requires max C <= 65535 (else *status_dev = DPS_ERR_OVERFLOW).  Entry order
@@ -475,6 +487,35 @@ int dps_row_scores(const int64_t* m, const int64_t* g, int64_t gx, int64_t n, do
 int dps_pair_count(const int32_t* a_col, const int32_t* a_val, int64_t a_len,
                    const int32_t* b_col, const int32_t* b_val, int64_t b_len,
                    int64_t* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Row sharding across ranks (no counterpart in the reference,
+ * whose Spark session :146-168 brings each .count() of :86/:107 back to the
+ * driver).  Device arrays, enqueued on `stream`, nothing read back:
+ * dps_shard_edges: contiguous shards of (nearly) equal work for `world` ranks:
+ *   work[i] = terms[i] + (sum(terms) / n_rows) / 2 (terms = the build's row
+ *   work, dps_walks_fused), edges[r] (int64 [world + 1]) = the number of rows
+ *   whose inclusive work prefix is <= r * total / world (edges[0] = 0,
+ *   edges[world] = n_rows).  With edges_ref, *mismatch += the number of r with
+ *   edges[r] != edges_ref[r] (a plan check inside a timed step).  1 <= world
+ *   <= 255; ws from dps_shard_edges_workspace_size(n_rows).
+ * dps_pack_counts: out[i] = (cnt[i] << 32) | (uint32)idx[i], the 8-byte wire
+ *   word of one top-k slot (the root rebuilds the score).
+ * dps_unpack_gathered: rows x in [edges[0], edges[world]) of the gathered
+ *   [world * m, k] words (rank r's rows at r * m), x at gathered row r * m +
+ *   x - edges[r]: out_idx / out_cnt [n_rows, k] and out_score = double(2 cnt) /
+ *   double(den[x] + den[idx]) -- the hot kernel's division of the same exact
+ *   integers (:51-52), bit-identical -- 0.0 for empty (-1) or zero-count slots.
+ *   n_rows must equal edges[world] - edges[0].
+ * ------------------------------------------------------------------------- */
+size_t dps_shard_edges_workspace_size(int64_t n_rows);
+int dps_shard_edges(const int64_t* terms, int64_t n_rows, int32_t world, int64_t* edges,
+                    const int64_t* edges_ref, int64_t* mismatch, void* ws, size_t ws_bytes,
+                    void* stream);
+int dps_pack_counts(const int32_t* idx, const int64_t* cnt, int64_t n, int64_t* out, void* stream);
+int dps_unpack_gathered(const int64_t* gathered, int32_t world, int64_t m, int32_t k,
+                        const int64_t* edges, int64_t n_rows, const int64_t* den, int32_t* out_idx,
+                        int64_t* out_cnt, double* out_score, void* stream);
 
 /* ---------------------------------------------------------------------------
  * RCCL over xGMI: one rank per process and GPU.  Replaces

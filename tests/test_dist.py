@@ -132,6 +132,80 @@ def test_compact_rescore_matches_kernel_division():
     assert np.array_equal(s2.numpy().view(np.int64), os_.view(np.int64))
 
 
+@pytest.mark.parametrize("world", [1, 2, 5, 8])
+def test_shard_edges_host_equals_row_work_plan(world):
+    """shard_edges(terms) (bench.py's plan over the build's row work terms)
+    equals balanced_edges over PathSimEngine.row_work() = terms + half the mean."""
+    from dpathsim.dist import balanced_edges, shard_edges
+    rng = np.random.default_rng(11 + world)
+    terms = torch.from_numpy(rng.pareto(1.1, 40_000).astype(np.int64) * 100)
+    work = terms + (terms.sum() // terms.numel()) // 2
+    assert shard_edges(terms, world).tolist() == balanced_edges(work, world).tolist()
+    ref = shard_edges(terms, world)
+    mism = torch.zeros(1, dtype=torch.int64)
+    shard_edges(terms, world, ref=ref, mismatch=mism)
+    assert int(mism) == 0
+    shard_edges(terms + 7 * (torch.arange(terms.numel()) % 3 == 0), world, ref=ref, mismatch=mism)
+    assert world == 1 or int(mism) >= 0
+    assert shard_edges(torch.zeros(0, dtype=torch.int64), world).tolist() == [0] * (world + 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3, 8, 255])
+def test_shard_edges_device_equals_host(world):
+    """dps_shard_edges (HIP) gives the host plan's edges bit for bit and counts
+    the edges that differ from a reference plan."""
+    from dpathsim.dist import shard_edges
+    rng = np.random.default_rng(world)
+    for n in (1, 7, 1000, 300_001):
+        terms = torch.from_numpy(rng.pareto(1.2, n).astype(np.int64) * 50)
+        host = shard_edges(terms, world)
+        dev = shard_edges(terms.cuda(), world)
+        assert dev.cpu().tolist() == host.tolist(), n
+        mism = torch.zeros(1, dtype=torch.int64, device="cuda")
+        shard_edges(terms.cuda(), world, ref=dev, mismatch=mism)
+        assert int(mism.item()) == 0
+        bad = dev.clone()
+        if world > 1:
+            bad[1] += 1
+            shard_edges(terms.cuda(), world, ref=bad, mismatch=mism)
+            assert int(mism.item()) == 1
+    z = shard_edges(torch.zeros(0, dtype=torch.int64, device="cuda"), world)
+    assert z.cpu().tolist() == [0] * (world + 1)
+
+
+@pytest.mark.gpu
+def test_pack_unpack_gathered_device():
+    """dps_pack_counts / dps_unpack_gathered (HIP) against the host PyTorch
+    words and rescore: shards of unequal size in a [world * m, k] buffer, -1
+    slots and zero counts, rows in order, scores bit for bit."""
+    from dpathsim.dist import pack_counts, rescore, unpack_gathered
+    rng = np.random.default_rng(5)
+    na, k, world = 5000, 7, 3
+    den = torch.from_numpy(rng.integers(1, 10 ** 9, na).astype(np.int64))
+    idx = torch.from_numpy(rng.integers(-1, na, (na, k)).astype(np.int32))
+    cnt = torch.from_numpy(rng.integers(0, 2 ** 31 - 1, (na, k)).astype(np.int64))
+    cnt[idx < 0] = 0
+    cnt[::11, 0] = 0
+    host_words = pack_counts(idx, cnt)
+    dev_words = pack_counts(idx.cuda(), cnt.cuda())
+    assert torch.equal(dev_words.cpu(), host_words)
+    edges = [0, 1200, 1200 + 2100, na]                  # shard sizes 1200, 2100, 1700
+    m = 2100
+    g = torch.full((world * m, k), -12345, dtype=torch.int64)
+    for r in range(world):
+        g[r * m: r * m + edges[r + 1] - edges[r]] = host_words[edges[r]:edges[r + 1]]
+    ei = torch.tensor(edges, dtype=torch.int64, device="cuda")
+    di, dc, ds = unpack_gathered(g.cuda(), world, m, ei, den.cuda())
+    hi, hc, hs = rescore(host_words, den, 0)
+    assert torch.equal(di.cpu(), hi) and torch.equal(dc.cpu(), hc)
+    assert torch.equal(ds.cpu().view(torch.int64), hs.view(torch.int64))
+    # a row range that does not start at 0 (a rank's slice, world 1)
+    si, sc_, ss = rescore(dev_words[300:900], den.cuda(), 300)
+    hi, hc, hs = rescore(host_words[300:900], den, 300)
+    assert torch.equal(si.cpu(), hi) and torch.equal(ss.cpu().view(torch.int64), hs.view(torch.int64))
+
+
 def test_pack_roundtrip():
     rng = np.random.default_rng(0)
     idx = torch.from_numpy(rng.integers(-1, 2 ** 31 - 1, (50, 7)).astype(np.int32))
@@ -151,20 +225,34 @@ def _engine_worker(rank, world, port, k, result_path):
         import pathsim_oracle as po
         from dpathsim.engine import build_engine
         from dpathsim.synth import synth_dblp
-        from dpathsim.dist import pack_counts
-        t = synth_dblp(30000, 90000, 300, seed=21).typed()
-        eng = build_engine(t, device="cuda:0", tile_w=8192)      # the bench shape
+        from dpathsim.dist import pack_counts, shard_edges
+        from dpathsim.synth import synth_config
+        # the bench shape: config3 at 1/20 scale (4 tiles of 16384), engine
+        # defaults -- auto W = 16384, venue skipping, companion half tiles
+        t = synth_config("config3", scale=0.05).typed()
+        eng = build_engine(t, device="cuda:0")
+        assert eng.tile_w == 16384 and eng.venue_skip and eng.half_tiles
         na = t.n_authors
-        bounds = balanced_bounds(eng.row_work(), world)
+        # bench.py's plan: dps_shard_edges over the build's row work (HIP), the
+        # same edges as the PyTorch plan over row_work()
+        edges = shard_edges(eng.tensor("row_terms")[:na], world)
+        e = edges.cpu().tolist()
+        bounds = [(e[r], e[r + 1]) for r in range(world)]
+        assert bounds == balanced_bounds(eng.row_work(), world)
+        mism = torch.zeros(1, dtype=torch.int64, device=eng.device)
+        shard_edges(eng.tensor("row_terms")[:na], world, ref=edges, mismatch=mism)
+        assert int(mism.item()) == 0
         r0, r1 = bounds[rank]
         m = max_shard(na, world, bounds)
         out = tuple(torch.zeros((m, k), dtype=dt, device=eng.device)
                     for dt in (torch.int32, torch.int64, torch.float64))
         eng.topk(k, r0, r1, out=tuple(o[: r1 - r0] for o in out))
         res = gather_topk(out, na, world, bounds=bounds)
-        # bench.py's wire path: 8-byte (count, index) words, rescored on rank 0
+        # bench.py's wire path: 8-byte (count, index) words (dps_pack_counts),
+        # rows reordered and rescored on rank 0 (dps_unpack_gathered)
         packed = pack_counts(out[0], out[1])
-        res8 = gather_topk_compact(packed, eng.tensor("den")[:na], na, world, bounds=bounds)
+        res8 = gather_topk_compact(packed, eng.tensor("den")[:na], na, world, bounds=bounds,
+                                   edges=edges)
         if rank == 0:
             fi, fc, fs = po.COracle.from_typed(t).topk(k, 0, na)
             ok = True
