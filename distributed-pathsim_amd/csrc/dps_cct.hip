@@ -550,16 +550,14 @@ __global__ __launch_bounds__(256) void k_dequeue_list(const uint32_t* __restrict
 // After the band pass (sym = 1): a row is "strong" when its band list holds k
 // positive scores; its k-th score, rounded down to fp32, is the threshold other
 // rows hand pairs on at (tau_emit, by target label; +inf: the row scans every
-// tile itself and takes no records), tau_blk the minimum over 2048 labels.
-// work = the C^T words the rest pass will read for the row plus a fixed cost per
-// accumulator pass (its heavy-first order).
-constexpr int64_t kSymPassCost = 2048;
+// tile itself and takes no records), tau_blk the minimum over 2048 labels,
+// tau_tile over a tile.  (The rest pass runs in descending label order,
+// k_desc_order, not heavy-first: a row's far targets have then mostly
+// published their own k-th scores.)
 __global__ __launch_bounds__(256) void k_sym_plan(
-    int64_t n, int k, int band, int shift, int64_t T, const int32_t* __restrict__ t_rank,
-    const double* __restrict__ band_score, const int64_t* __restrict__ c_ptr,
-    const int32_t* __restrict__ c_col, const uint32_t* __restrict__ tile_off,
-    uint8_t* __restrict__ strong, float* __restrict__ tau_emit, uint32_t* __restrict__ tau_blk,
-    uint32_t* __restrict__ tau_tile, int64_t* __restrict__ work) {
+    int64_t n, int k, int shift, const int32_t* __restrict__ t_rank,
+    const double* __restrict__ band_score, uint8_t* __restrict__ strong,
+    float* __restrict__ tau_emit, uint32_t* __restrict__ tau_blk, uint32_t* __restrict__ tau_tile) {
   for (int64_t x = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; x < n;
        x += static_cast<int64_t>(gridDim.x) * 256) {
     const double kth = band_score[x * k + k - 1];
@@ -572,14 +570,6 @@ __global__ __launch_bounds__(256) void k_sym_plan(
       atomicMin(&tau_blk[lx >> 11], __float_as_uint(te));
       atomicMin(&tau_tile[lx >> shift], __float_as_uint(te));
     }
-    const int64_t a = lx >> shift;
-    const int64_t t0 = st ? (a + band + 1 < T ? a + band + 1 : T) : 0;
-    int64_t w = 0;
-    for (int64_t j = c_ptr[x]; j < c_ptr[x + 1]; ++j) {
-      const int64_t v = c_col[j];
-      w += static_cast<int64_t>(tile_off[(v + 1) * T]) - static_cast<int64_t>(tile_off[v * T + t0]);
-    }
-    work[x] = w + (T - t0) * kSymPassCost;
   }
 }
 
@@ -810,6 +800,7 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   p.h_ent = half ? ext->half_ent : nullptr;
   p.h_maxc = half ? (tile_maxc ? ext->half_maxc : ext->half_off) : nullptr;
   p.T8 = (n_targets + 8191) / 8192;
+  p.tile_sum = half ? ext->tile_sum : nullptr;
   p.c_ptr = c_ptr; p.c_col = c_col; p.c_val = c_val;
   p.g = g; p.g_t = g_t ? g_t : g; p.t_perm = t_perm; p.t_rank = t_rank;
   p.tile_off = tile_off; p.tile_ent = tile_ent; p.tile_gmin = tile_gmin;
@@ -867,8 +858,8 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   if (kProfile)
     if (const char* ab = std::getenv("DPATHSIM_ABLATE")) p.ablate = std::atoi(ab);
   // word 0: row dequeue counter; words 1-3: the lean kernel's pass / chunk /
-  // table-completed candidate counts
-  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : 4 * sizeof(unsigned long long), st));
+  // table-completed candidate counts, word 4 its overflowed optimistic passes
+  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : 8 * sizeof(unsigned long long), st));
   // the bench shape (W = 8192, one wave per row) runs the lean kernel
   // (dps_cct1.hip); DPATHSIM_LEAN=0 selects this file's general kernel
   bool lean = (shift == 13 || shift == 14) && nw == 1 && (p.ablate == 0 || p.ablate == 16);
@@ -944,9 +935,9 @@ size_t dps_cct_sym_workspace_size(int64_t n_targets, int32_t k, int64_t rec_cap)
   const size_t cap = static_cast<size_t>(rec_cap > 0 ? rec_cap : 1);
   size_t b = 0;
   b += align_up(nk * 4) + align_up(nk * 8) + align_up(nk * 8);   // rest lists
-  b += align_up(n) + align_up(n * 4) + align_up((n / 2048 + 2) * 4) + align_up(n * 8);
+  b += align_up(n) + align_up(n * 4) + align_up((n / 2048 + 2) * 4);   // strong, tau_emit, tau_blk
   b += 2 * align_up((n + 1) * 4) + align_up((n / 2048 + 2) * 4);   // tau_tile, tile_done, blk_done
-  b += align_up(n * 4) + align_up(dps_heavy_first_workspace_size(n_targets));
+  b += align_up(n * 4);                                          // rest-pass order
   b += 5 * align_up(cap * 4);                                    // records + placed records
   b += align_up(8) + 2 * align_up((n + 1) * 4) + align_up((n + 1) * 8);
   b += align_up(scan_workspace_size(n_targets + 1)) + align_up(256);
@@ -990,10 +981,7 @@ int dps_cct_sym(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val
   uint32_t* tau_tile = c.take<uint32_t>(T + 1);
   uint32_t* blk_done = c.take<uint32_t>(n / 2048 + 2);
   uint32_t* tile_done = c.take<uint32_t>(T + 1);
-  int64_t* work = c.take<int64_t>(n);
   int32_t* dq = c.take<int32_t>(n);
-  const size_t hf_bytes = dps_heavy_first_workspace_size(n);
-  void* hf = c.take<char>(hf_bytes);
   int32_t* rec_y = c.take<int32_t>(rec_cap);
   int32_t* rec_x = c.take<int32_t>(rec_cap);
   int32_t* rec_m = c.take<int32_t>(rec_cap);
@@ -1027,17 +1015,14 @@ int dps_cct_sym(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val
                          out_cnt, out_score, band_ctr, 256, stream, 0, nullptr, nullptr, nullptr,
                          nullptr, nullptr, &sy);
   if (rc != DPS_OK) return rc;
-  // 2. plan: strong rows, emission thresholds, rest-pass work and order
-  k_sym_plan<<<grid_for(n, 256), 256, 0, st>>>(n, k, band, shift, T, t_rank, out_score, c_ptr,
-                                                 c_col, tile_off, strong, tau_emit, tau_blk,
-                                                 tau_tile, work);
+  // 2. plan: strong rows and the emission thresholds
+  k_sym_plan<<<grid_for(n, 256), 256, 0, st>>>(n, k, shift, t_rank, out_score, strong, tau_emit,
+                                                 tau_blk, tau_tile);
   DPS_LAUNCHED();
   // rest pass in descending label order: a row's far targets (higher labels)
   // have mostly finished and published their own k-th scores by then
   k_desc_order<<<grid_for(n, 256), 256, 0, st>>>(t_perm, n, dq);
   DPS_LAUNCHED();
-  (void)hf;
-  (void)hf_bytes;
   // 3. rest pass: records for the pairs only this row sees
   sy.sym = 2;
   sy.row_strong = strong;

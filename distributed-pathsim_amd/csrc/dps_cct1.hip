@@ -89,6 +89,31 @@ template <> struct Fmt<2> {
 #endif
 constexpr int kEpi1 = DPS_EPI1;                // epilogue blocks read per trip
 
+// Optimistic 4-bit pass check: the digit sum of the nibbles of each half of
+// the 8 KiB accumulator (blocks 0-3 = targets 0..8191, blocks 4-7; one
+// v_dot8_u32_u4 with 0x11111111 per dword) equals exp_a / exp_b exactly when
+// no count of that half carried out of its nibble (see kOptMax).  Returns the
+// epilogue's block mask: bits 0-3 when half a is good, 4-7 when half b is.
+__device__ __forceinline__ uint32_t opt_check(const uint32_t* acc, uint32_t exp, int lane) {
+  const uint32_t exp_a = exp & 0xFFFFu, exp_b = exp >> 16;   // 0xFFFF: saturated, never equal
+  uint32_t sa = 0, sb = 0;
+#pragma unroll 2
+  for (int b0 = 0; b0 < kAcc1 / 2; b0 += kWave * 4) {
+    const uint4 a = *reinterpret_cast<const uint4*>(acc + b0 + lane * 4);
+    const uint4 b = *reinterpret_cast<const uint4*>(acc + kAcc1 / 2 + b0 + lane * 4);
+    sa = __builtin_amdgcn_udot8(a.x, 0x11111111u, sa, false);
+    sa = __builtin_amdgcn_udot8(a.y, 0x11111111u, sa, false);
+    sa = __builtin_amdgcn_udot8(a.z, 0x11111111u, sa, false);
+    sa = __builtin_amdgcn_udot8(a.w, 0x11111111u, sa, false);
+    sb = __builtin_amdgcn_udot8(b.x, 0x11111111u, sb, false);
+    sb = __builtin_amdgcn_udot8(b.y, 0x11111111u, sb, false);
+    sb = __builtin_amdgcn_udot8(b.z, 0x11111111u, sb, false);
+    sb = __builtin_amdgcn_udot8(b.w, 0x11111111u, sb, false);
+  }
+  return (exp_a != 0xFFFFu && wave_sum_u32(sa) == exp_a ? 0x0Fu : 0u) |
+         (exp_b != 0xFFFFu && wave_sum_u32(sb) == exp_b ? 0xF0u : 0u);
+}
+
 // Zero the kEpi1 KiB of accumulator an epilogue trip has just read (dwords
 // b0..).  (ds_write_addtid_b32 zeroes 1.46x faster in isolation,
 // tools/ubench/addtid.hip, but did not move the kernel: DESIGN.md §6.)
@@ -97,6 +122,21 @@ __device__ __forceinline__ void zero_trip(uint32_t* acc, int b0, int lane) {
   for (int i = 0; i < kEpi1; ++i)
     *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
 }
+
+// A kernel parameter read where it is used -- an s_load from the kernarg
+// segment each time (the kernel's only argument is the CctParams, at offset
+// 0) -- instead of being held in SGPRs, or spilled to VGPR lanes, across the
+// whole row loop: for the fields only the per-row code needs.  The asm
+// launders the base so the loads cannot be hoisted back out of the loop.
+// (Taking p's address instead would copy the struct to scratch.)
+template <class T>
+__device__ __forceinline__ T kcold_at(size_t off) {
+  typedef const __attribute__((address_space(4))) char* kb;
+  kb base = (kb)(__builtin_amdgcn_kernarg_segment_ptr());
+  asm volatile("" : "+s"(base));
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(base + off);
+}
+#define kcold(field) kcold_at<decltype(CctParams::field)>(offsetof(CctParams, field))
 
 // Symmetric rest pass: the bounds other rows raise are read with plain loads
 // (any value read is a valid bound; an atomic load would wait for every
@@ -226,18 +266,50 @@ struct Pend1 {
   int t;         // tile (u8h: a half tile of the companion W = 8192 set)
   uint32_t ub;
   bool u8h;
+  bool opt;      // optimistic 4-bit pass over a tile whose bound exceeds 15 (see kOptMax)
+  uint32_t hb;   // opt: the tile's two half bounds (Win1::hb), for the redo
   uint32_t lo, hi;
   uint32_t mx;   // venue skipping: max C[y,v] over the tile's targets (lane = venue)
+  uint32_t hs;   // opt: the count sums of the venue's buckets in the two u8 halves
+                 // (tile_sum of the companion tiles), 16 bits each, saturated
   int64_t gs;
   float tb;      // symmetric rest pass, far tile: lane s < 8, min tau_emit over segment s
 };
 
+// Optimistic 4-bit passes (round 4).  A 16384-target tile whose 4-bit bound
+// exceeds 15 used to run as its two u8 halves (two accumulator passes, 24 % of
+// all passes on config3), but the bound is loose: most such tiles have no
+// target with 16 or more paths (tools/sim_overflow.py).  Such a tile now takes
+// ONE 4-bit pass, and a nibble that overflowed is detected exactly before
+// anything is read from the accumulator: a count c >= 16 carries into the next
+// nibble (or out of the dword), which lowers the sum of the nibble digits by 15
+// (16) per carry, so the digit sum of a half's 4 KiB of counters
+// (v_dot8_u32_u4 against 0x11111111, one VALU per dword) equals
+// sum_{v scattered} C[x,v] * tile_sum[v, half] -- the sum of the half's counts
+// -- if and only if none of its counts reached 16.  Carries never cross the
+// halves (a dword holds 8 consecutive labels), so each half is judged alone: a
+// good half goes through the epilogue, a bad one is cleared and queued to run
+// again as its u8 half tile (the old path).  Results are exact either way.
+// Tiles whose bound exceeds kOptMax, rows with more than 64 venues and the
+// symmetric mode split as before.
+#ifndef DPS_OPT_MAX
+#define DPS_OPT_MAX 255
+#endif
+#ifndef DPS_OPT_INEPI
+#define DPS_OPT_INEPI 0   // 1: judge each half inside the epilogue (no separate read)
+#endif
+constexpr uint32_t kOptMax = DPS_OPT_MAX;   // 0 = off
+constexpr uint32_t kOptSumMax = 0xFFFFu;    // bucket sums above this: no opt pass
+
 template <int F, bool HV, bool SY>
 __device__ __forceinline__ void pend_load(const CctParams& p, Pend1& P, int t, uint32_t ub, bool u8h,
-                                          int d0, uint32_t vT, uint32_t vT8, int lane, int far) {
+                                          int d0, uint32_t vT, uint32_t vT8, int lane, int far,
+                                          bool opt = false, uint32_t hb = 0) {
   P.t = t;
   P.ub = ub;
   P.u8h = u8h;
+  P.opt = opt;
+  P.hb = hb;
   P.lo = P.hi = 0;
   P.mx = 0;
   P.gs = 0;
@@ -249,6 +321,13 @@ __device__ __forceinline__ void pend_load(const CctParams& p, Pend1& P, int t, u
     P.lo = off[b];
     P.hi = off[b + 1u];
     if (HV) P.mx = p.use_bounds ? (u8h ? p.h_maxc : p.tile_maxc)[b] : 0xFFFFu;
+    P.hs = 0;
+    if (opt) {                  // the tile's halves 2t, 2t+1 in the companion set
+      const uint32_t b8 = vT8 + 2u * static_cast<uint32_t>(t);
+      const uint32_t sa = p.tile_sum[b8];
+      const uint32_t sb = 2 * t + 1 < p.T8 ? p.tile_sum[b8 + 1u] : 0u;
+      P.hs = (sa < kOptSumMax ? sa : kOptSumMax) | ((sb < kOptSumMax ? sb : kOptSumMax) << 16);
+    }
   }
   if (lane < 8) {
     const int sh = u8h ? Fmt<1>::S : Fmt<F>::S, sg = u8h ? Fmt<1>::SEG : Fmt<F>::SEG;
@@ -263,6 +342,10 @@ struct Stage1 {
   float gsf;     // lane s < 8: smallest g of segment s, as float
   float tbf;     // lane s < 8: symmetric rest pass, min tau_emit of segment s (inf: none)
   bool u8h;      // a u8 half tile of the companion set (F = 2, dual)
+  bool opt;      // optimistic 4-bit pass (Pend1::opt)
+  uint32_t hb;   // opt: half bounds for the redo
+  uint32_t exp;  // opt: each half's digit sum when none of its counts reached 16, 16 bits
+                 // each (saturated at 0xFFFF: the check then fails, both halves run again)
   int ubh;       // venue skipping: sum_{h in H} C[x,h] * maxc[h, tile] >= M_H of any target
 };
 
@@ -272,12 +355,28 @@ __device__ __forceinline__ void stage_make(Stage1& X, const Pend1& P, int c, int
                                            int lane) {
   X.S.t = P.t;
   X.u8h = P.u8h;
+  X.opt = P.opt;
+  X.hb = P.hb;
   // log2 of the passes: counters of BITS << lnp bits must hold the bound
   if (F == 1 || P.u8h) X.S.lnp = P.ub <= 0xFFu ? 0 : P.ub <= 0xFFFFu ? 1 : 2;
-  else X.S.lnp = P.ub <= 0xFu ? 0 : P.ub <= 0xFFu ? 1 : P.ub <= 0xFFFFu ? 2 : 3;
+  else X.S.lnp = P.ub <= 0xFu || P.opt ? 0 : P.ub <= 0xFFu ? 1 : P.ub <= 0xFFFFu ? 2 : 3;
   X.S.pass = 0;
   const bool skip = (hm >> lane) & 1ull;          // an H venue's bucket is not scattered
   grp_set(X.S.G, P.lo, skip ? P.lo : P.hi, c, d0);
+  X.exp = 0;
+  if (P.opt) {
+    // sum of the counts the scatter adds to each half: C[x,v] * (count sum of
+    // the venue's bucket in that half) over the scattered venues; above 8192 *
+    // 15 some count must exceed 15, so the check is made to fail (saturated
+    // sums do the same)
+    auto part = [&](uint32_t sm) -> uint32_t {
+      const uint64_t pr64 = skip ? 0ull : static_cast<uint64_t>(c) * sm;
+      return sm >= kOptSumMax || pr64 > 0xFFFFull ? 0xFFFFu : static_cast<uint32_t>(pr64);
+    };
+    const uint32_t ea = wave_sum_u32(part(P.hs & 0xFFFFu));
+    const uint32_t eb = wave_sum_u32(part(P.hs >> 16));
+    X.exp = (ea < 0xFFFFu ? ea : 0xFFFFu) | ((eb < 0xFFFFu ? eb : 0xFFFFu) << 16);
+  }
   X.ubh = 0;
   if (hm) {
     // c, mx <= 65535: the product fits 32 bits; a product beyond 16 bits makes
@@ -307,7 +406,9 @@ __device__ __forceinline__ void sort_venues(const CctParams& p, int d0, int lane
     const uint32_t n = p.tile_off[vT + static_cast<uint32_t>(p.T)] - p.tile_off[vT];
     key = static_cast<int>((n < (1u << 24) ? n : (1u << 24) - 1u) << 6) | lane;
   }
-  const int src = wave_bitonic_sort(key) & (kWave - 1);
+  // (the network's lane masks rebuilt per row: hoisted, they held 42 SGPRs for
+  // the whole kernel and pushed ~250 SGPR spills into the stage loop)
+  const int src = wave_bitonic_sort(key, opaque_lane(lane)) & (kWave - 1);
   c = __shfl(c, src, kWave);
   vT = static_cast<uint32_t>(__shfl(static_cast<int>(vT), src, kWave));
   if (HV) v = __shfl(v, src, kWave);
@@ -331,6 +432,7 @@ __device__ __forceinline__ float hv_ratio(uint32_t hv) { return __uint_as_float(
 // of the symmetric mode, the row and the first tile whose pairs it hands on.
 struct RowAux {
   uint32_t ver = 0, cand = 0, ins = 0;
+  uint32_t redo = 0;            // optimistic 4-bit passes that overflowed (counter[4])
   uint32_t u8h = 0, wide = 0;   // profiling build: half-tile and wide passes
   int x = 0;               // source row (ordinal)
   int far = INT_MAX;       // sym = 2: targets in tiles >= far may go to records
@@ -506,15 +608,22 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
 template <int KPL, bool HV, bool SY>
 __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                         int t, int lane, int64_t x_lab, int64_t gx, int mseg,
-                                        int c, uint32_t hv, uint64_t hm, RowAux& ra) {
+                                        int c, uint32_t hv, uint64_t hm, RowAux& ra,
+                                        uint32_t bmask, uint32_t oexp, uint32_t& bad) {
   constexpr int kS = Fmt<2>::S, kSeg = Fmt<2>::SEG;
   const int64_t tile_base = static_cast<int64_t>(t) << kS;
   const int64_t xr = x_lab - tile_base;
   const bool xin = xr >= 0 && xr < (int64_t(1) << kS);   // the source is a target of this tile
   const int xrel = xin ? static_cast<int>(xr) : 0;
+  // optimistic pass judged here (oexp != 0, DPS_OPT_INEPI): each half's
+  // candidates are held in the queue (no flush) until its digit sum shows no
+  // overflowed count; a bad half's candidates are dropped (Q.n back to snap)
+  bool hold = oexp != 0u, abort = false;
+  uint32_t dsum = 0;
+  int snap = Q.n;
   auto block = [&](uint4 a, int blk) {
     const uint32_t m = static_cast<uint32_t>(readlane(mseg, blk));
-    if (m > 15u) return;                           // no 4-bit count reaches m
+    if (m > 15u || !((bmask >> blk) & 1u)) return;   // no 4-bit count reaches m / overflowed half
     const uint32_t pm = (0x10u - (0x80000000u >> __builtin_clz(m))) * 0x11111111u;
     if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) return;
     // target (8*dw + nib) of this lane's 32 -> bit 4*nib + 3 - dw
@@ -554,7 +663,13 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
         mv = static_cast<int>((wv >> (nib * 4)) & 0xFu);
       }
       vq_push(Q, has, lab, mv, mk, lane);
-      if (Q.n >= kWave) vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
+      if (Q.n >= kWave) {
+        if (hold) {         // an unverified half may not be flushed: give it up
+          abort = true;
+          return;
+        }
+        vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
+      }
     }
   };
 #pragma unroll 1
@@ -565,7 +680,34 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
       a[i] = *reinterpret_cast<const uint4*>(acc + b0 + i * kWave * 4 + lane * 4);
     zero_trip(acc, b0, lane);
 #pragma unroll
-    for (int i = 0; i < kEpi1; ++i) block(a[i], (b0 >> 8) + i);
+    for (int i = 0; i < kEpi1; ++i) {
+      const int blk = (b0 >> 8) + i;
+      if (hold) {            // optimistic pass: the digit sum of this half so far
+        dsum = __builtin_amdgcn_udot8(a[i].x, 0x11111111u, dsum, false);
+        dsum = __builtin_amdgcn_udot8(a[i].y, 0x11111111u, dsum, false);
+        dsum = __builtin_amdgcn_udot8(a[i].z, 0x11111111u, dsum, false);
+        dsum = __builtin_amdgcn_udot8(a[i].w, 0x11111111u, dsum, false);
+      }
+      if (!abort) block(a[i], blk);
+      if (hold && (blk & 3) == 3) {
+        // end of a half: its candidates stand only if no count overflowed
+        const uint32_t e = blk == 3 ? (oexp & 0xFFFFu) : (oexp >> 16);
+        const bool ok = !abort && e != 0xFFFFu && wave_sum_u32(dsum) == e;
+        if (!ok) {
+          Q.n = snap;
+          bad |= blk == 3 ? 1u : 2u;
+        }
+        dsum = 0;
+        abort = false;
+        snap = Q.n;
+        if (Q.n >= kWave) {
+          hold = false;
+          vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
+          hold = true;
+          snap = Q.n;
+        }
+      }
+    }
   }
 }
 
@@ -793,19 +935,22 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
 
   for (;;) {
     unsigned long long rr = 0;
-    if (lane == 0) rr = atomicAdd(p.counter, 1ull);
+    if (lane == 0) rr = atomicAdd(kcold(counter), 1ull);
     const int64_t r = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rr)));
-    if (r >= p.n_rows) break;
-    const int64_t x = p.row_order ? static_cast<int64_t>(p.row_order[r]) : p.row_begin + r;
-    const bool is_piece = r < p.n_pieces;
-    const int64_t ro = (is_piece || p.out_by_slot) ? r : x - p.row_begin;
-    int t_beg = is_piece ? p.piece_t0[r] : 0;
-    int t_end = is_piece ? p.piece_t1[r] : static_cast<int>(p.T);
+    if (r >= kcold(n_rows)) break;
+    const int32_t* row_order = kcold(row_order);
+    const int64_t x = row_order ? static_cast<int64_t>(row_order[r]) : kcold(row_begin) + r;
+    const bool is_piece = r < kcold(n_pieces);
+    const int64_t ro = (is_piece || kcold(out_by_slot)) ? r : x - kcold(row_begin);
+    int t_beg = is_piece ? kcold(piece_t0)[r] : 0;
+    int t_end = is_piece ? kcold(piece_t1)[r] : static_cast<int>(p.T);
     DPS_DASSERT(0 <= t_beg && t_beg <= t_end && t_end <= p.T);
-    const int64_t x_lab = p.t_rank ? static_cast<int64_t>(p.t_rank[x]) : x;
-    const int64_t pb = p.c_ptr[x];
-    const int d = static_cast<int>(p.c_ptr[x + 1] - pb);
-    const int64_t gx = p.g[x];
+    const int32_t* t_rank = kcold(t_rank);
+    const int64_t x_lab = t_rank ? static_cast<int64_t>(t_rank[x]) : x;
+    const int64_t* c_ptr = kcold(c_ptr);
+    const int64_t pb = c_ptr[x];
+    const int d = static_cast<int>(c_ptr[x + 1] - pb);
+    const int64_t gx = kcold(g)[x];
     const float gxf = i64_f32(gx);
     TopK<KPL> top;
     top.init(p.k);
@@ -833,8 +978,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       int c = 0, v = 0;
       uint32_t vT = 0;
       if (lane < d0) {
-        c = p.c_val[pb + lane];
-        v = p.c_col[pb + lane];
+        c = kcold(c_val)[pb + lane];
+        v = kcold(c_col)[pb + lane];
         vT = static_cast<uint32_t>(v) * static_cast<uint32_t>(p.T);
       }
       if (d0 > 1) sort_venues<HV || F == 2>(p, d0, lane, c, vT, v);
@@ -849,10 +994,22 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       auto half_ub = [&](uint32_t h, uint32_t ub4) -> uint32_t {
         return h >= kHalfSat ? ub4 : h;
       };
-      // next stage: the pending half, else the next live tile -- split into its
-      // two u8 halves when dual and its 4-bit bound exceeds 15
-      auto choose = [&](double tau, int& tn, uint32_t& ubn, bool& u8n) {
+      // next stage: the pending half, else the next live tile -- when dual and
+      // its 4-bit bound exceeds 15, an optimistic 4-bit pass (opt) or, above
+      // kOptMax, its two u8 halves
+      const bool opt_ok = !SY && kOptMax > 0 && dual && p.tile_sum != nullptr && d <= kWave;
+      // the u8 halves of an overflowed opt tile, queued (they run after the
+      // prefetched next stage: tiles may be visited in any order)
+      // (t8 << 8 | bound, bound <= kOptMax <= 255).  At most four: a check
+      // runs after its stage's transition, when the next two stages are
+      // already chosen -- each of those may push two more -- and from then on
+      // choose() pops one per stage and a half never overflows.
+      uint32_t rq[4] = {0, 0, 0, 0};
+      int rq_n = 0;
+      auto choose = [&](double tau, int& tn, uint32_t& ubn, bool& u8n, bool& optn, uint32_t& hbo) {
         u8n = false;
+        optn = false;
+        hbo = 0;
         if (h_next >= 0) {
           tn = h_next;
           ubn = h_ub;
@@ -860,9 +1017,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
           h_next = -1;
           return;
         }
+        if (rq_n > 0) {           // u8 halves of an overflowed opt tile
+          tn = static_cast<int>(rq[0] >> 8);
+          ubn = rq[0] & 0xFFu;
+          u8n = true;
+          rq[0] = rq[1];
+          rq[1] = rq[2];
+          rq[2] = rq[3];
+          --rq_n;
+          return;
+        }
         uint32_t hbn = 0;
         tn = next_tile<SY>(p, w, t_end, pb, d, c, vT, vT8, dual, lane, tau, gxf, ubn, hbn, ra.far);
         if (!dual || tn < 0 || ubn <= Fmt<F>::UB0) return;
+        if (opt_ok && ubn <= kOptMax) {
+          optn = true;
+          hbo = hbn;
+          return;
+        }
         const int ta = 2 * tn, tb = 2 * tn + 1;
         const uint32_t ua = half_ub(hbn & 0xFFFFu, ubn);
         const uint32_t ubb = tb < p.T8 ? half_ub(hbn >> 16, ubn) : 0u;
@@ -881,27 +1053,27 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       uint32_t hv = 0;          // hv_pack(C[x,v] / s_v rounded up, slot)
       uint64_t hm = 0;          // H: venue lanes no longer scattered
       if (HV && lane < d0) {
-        const int sl = p.hv_slot[v];
+        const int sl = kcold(hv_slot)[v];
         if (sl >= 0)
-          hv = hv_pack(static_cast<float>(static_cast<double>(c) / static_cast<double>(p.s[v])) *
+          hv = hv_pack(static_cast<float>(static_cast<double>(c) / static_cast<double>(kcold(s)[v])) *
                            (1.0f + 0x1p-20f), sl);
       }
       win_load<SY>(p, w, t_beg, t_beg, t_end, pb, d, c, vT, vT8, dual, lane, -1.0, gxf, ra.far);
-      uint32_t ub_t = 0;
+      uint32_t ub_t = 0, hb_t = 0;
       int t0;
-      bool u8n;
-      choose(-1.0, t0, ub_t, u8n);
+      bool u8n, optn;
+      choose(-1.0, t0, ub_t, u8n, optn, hb_t);
       if (t0 >= 0) {
         Pend1 P;
-        pend_load<F, HV, SY>(p, P, t0, ub_t, u8n, d0, vT, vT8, lane, ra.far);
+        pend_load<F, HV, SY>(p, P, t0, ub_t, u8n, d0, vT, vT8, lane, ra.far, optn, hb_t);
         Stage1 X;
         stage_make<F>(X, P, c, d0, 0ull, lane);
         bool hchg = false;        // H grew at the last stage boundary
         Batch B;
         issue1(X.S, 0, X.u8h ? p.h_ent : p.tile_ent, lane, B);
         int t1;
-        choose(-1.0, t1, ub_t, u8n);
-        pend_load<F, HV, SY>(p, P, t1, ub_t, u8n, d0, vT, vT8, lane, ra.far);
+        choose(-1.0, t1, ub_t, u8n, optn, hb_t);
+        pend_load<F, HV, SY>(p, P, t1, ub_t, u8n, d0, vT, vT8, lane, ra.far, optn, hb_t);
         for (;;) {
           const int npass = 1 << X.S.lnp;
           bool more = false;
@@ -958,6 +1130,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
             const bool u8S = F == 1 || X.u8h;   // this stage's counters: u8 format
             const bool S_u8h = X.u8h;
             const uint64_t hmS = hm;   // this stage's H (the update below is for the next)
+            // optimistic 4-bit pass: did any count reach 16?  (then the
+            // accumulator is cleared and the tile's two u8 halves run next)
+            // optimistic 4-bit pass: judged after the transition below, so the
+            // next stage's first chunks are in flight during the check
+            // (S_hb != 0 for an opt stage: its bound exceeds 15, so one half's
+            // bound is positive; S_exp: the two halves' expected sums, 16 bits each)
+            const uint32_t S_hb = X.opt ? X.hb : 0u;
+            const uint32_t S_exp = X.exp;
             if (prof) ts[2] = __builtin_amdgcn_s_memtime();
             if (last) {
               // next stage: its bounds were loaded one stage ago; put its first
@@ -978,16 +1158,42 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
                   row_done = d <= kWave && hm == ballot(lane < d0);
                 }
               }
-              more = P.t >= 0 && !row_done;
-              if (more) stage_make<F>(X, P, c, d0, hm, lane);
-              else X.S.G.nq = 0;
+              // (an overflowed opt tile's halves are queued behind the
+              // prefetched P; when P ran out, one empty stage -- nothing
+              // scattered, an all-zero accumulator -- lets them load)
+              more = (P.t >= 0 || rq_n > 0) && !row_done;
+              if (more && P.t >= 0) {
+                stage_make<F>(X, P, c, d0, hm, lane);
+              } else {
+                X.S.G.nq = 0;
+                X.S.nb = 0;
+                X.S.lnp = 0;
+                X.opt = false;
+              }
               if (prof) ts[5] = __builtin_amdgcn_s_memtime();
               issue1(X.S, 0, X.u8h ? p.h_ent : p.tile_ent, lane, B);
               if (prof) ts[6] = __builtin_amdgcn_s_memtime();
               int tn = -1;
-              if (more) choose(tau, tn, ub_t, u8n);
-              pend_load<F, HV, SY>(p, P, tn, ub_t, u8n, d0, vT, vT8, lane, ra.far);
+              if (more) choose(tau, tn, ub_t, u8n, optn, hb_t);
+              pend_load<F, HV, SY>(p, P, tn, ub_t, u8n, d0, vT, vT8, lane, ra.far, optn, hb_t);
             }
+            // which halves of an optimistic pass have a count that reached 16?
+            // (the epilogue clears them without judging them; they run again
+            // as their u8 half tiles, queued for a later stage)
+            uint32_t bmask = 0xFFu, bad = 0u;
+#if DPS_OPT_INEPI
+            const uint32_t oexp = S_hb != 0u ? (S_exp == 0u ? 0xFFFFFFFFu : S_exp) : 0u;
+#else
+            const uint32_t oexp = 0u;
+            if (S_hb != 0u) {
+#ifdef DPS_EXP_NOCHECK
+              bmask = 0xFFu;       // experiment only: wrong results when a count overflows
+#else
+              bmask = opt_check(acc, S_exp, lane);
+#endif
+              bad = (bmask & 0x0Fu ? 0u : 1u) | (bmask & 0xF0u ? 0u : 2u);
+            }
+#endif
             if (prof) ts[3] = __builtin_amdgcn_s_memtime();
             if (S.lnp == 0) {
               if (u8S)
@@ -995,11 +1201,32 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
                                  hmS, ra);
               else
                 epi1_u4<KPL, HV, SY>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
-                                 hmS, ra);
+                                 hmS, ra, bmask, oexp, bad);
             } else if (u8S) {
               epi1_wide<1, KPL, HV, SY>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, ra);
             } else {
               epi1_wide<F, KPL, HV, SY>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, ra);
+            }
+            if (bad) {
+              // halves of an optimistic pass with a count that reached 16: run
+              // again as their u8 half tiles, queued for a later stage (half
+              // bounds <= the opt tile's bound <= kOptMax: never saturated)
+              ++ra.redo;
+              const int ta = 2 * static_cast<int>(S.t), tb = ta + 1;
+              const uint32_t ua = (bad & 1u) ? S_hb & 0xFFFFu : 0u;
+              const uint32_t ubb = (bad & 2u) && tb < p.T8 ? S_hb >> 16 : 0u;
+              auto push = [&](int t8, uint32_t u) {
+                const uint32_t e = (static_cast<uint32_t>(t8) << 8) | u;
+                if (rq_n == 0) rq[0] = e;
+                else if (rq_n == 1) rq[1] = e;
+                else if (rq_n == 2) rq[2] = e;
+                else rq[3] = e;
+                ++rq_n;
+              };
+              if (ua) push(ta, ua);
+              if (ubb) push(tb, ubb);
+              // the row had no stage left: one empty stage picks the halves up
+              if (rq_n > 0 && !more && X.S.G.nq == 0 && hm != ballot(lane < d0)) more = true;
             }
             // the queue holds counts that miss hmS: complete them before the
             // next stage's (larger) H applies
@@ -1024,9 +1251,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
     }
 
     // ranked entries, then zero-score targets in reference order, then -1
-    int32_t* oi = (is_piece ? p.piece_idx : p.out_idx) + ro * p.k;
-    int64_t* oc = (is_piece ? p.piece_cnt : p.out_cnt) + ro * p.k;
-    double* os = (is_piece ? p.piece_score : p.out_score) + ro * p.k;
+    const int kk = kcold(k);
+    int32_t* oi = (is_piece ? kcold(piece_idx) : kcold(out_idx)) + ro * kk;
+    int64_t* oc = (is_piece ? kcold(piece_cnt) : kcold(out_cnt)) + ro * kk;
+    double* os = (is_piece ? kcold(piece_score) : kcold(out_score)) + ro * kk;
 #pragma unroll
     for (int q = 0; q < KPL; ++q) {
       const int slot = q * kWave + lane;
@@ -1064,6 +1292,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
     atomicAdd(p.counter + 1, static_cast<unsigned long long>(n_pass));
     atomicAdd(p.counter + 2, static_cast<unsigned long long>(n_chunk));
     if (HV && ra.ver) atomicAdd(p.counter + 3, static_cast<unsigned long long>(ra.ver));
+    if (ra.redo) atomicAdd(p.counter + 4, static_cast<unsigned long long>(ra.redo));
   }
   if (prof && lane == 0) {
 #pragma unroll

@@ -60,6 +60,9 @@ struct CctParams {
   const uint32_t* h_ent;
   const uint32_t* h_maxc;
   int64_t T8;
+  // optimistic 4-bit passes (dps_cct1.hip, kOptMax): per-bucket count sums of
+  // the 16384-target tiles (dps_ct_tiles_sums); null = tiles above 15 split
+  const uint32_t* tile_sum;
   // symmetric mode (lean kernel, dps_cct_sym): M[x,y] = M[y,x],
   // so a pair is scanned once.  Row x in tile a = label(x) >> shift:
   //   sym = 1  band pass: tiles [a - band, a + band] only;

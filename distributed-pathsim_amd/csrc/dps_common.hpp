@@ -121,9 +121,11 @@ __device__ __forceinline__ int wave_owner(uint32_t excl, uint32_t i) {
   return j;
 }
 
-// Ascending bitonic sort of one int per lane across the wave.
-__device__ __forceinline__ int wave_bitonic_sort(int v) {
-  const int lane = lane_id();
+// Ascending bitonic sort of one int per lane across the wave.  `lane` is the
+// caller's lane id; a kernel that sorts inside a long-lived loop passes it
+// through opaque_lane() so that the 21 lane masks of the network are rebuilt
+// per call instead of being hoisted out of the loop into 42 SGPRs.
+__device__ __forceinline__ int wave_bitonic_sort(int v, int lane) {
 #pragma unroll
   for (int k = 2; k <= kWave; k <<= 1) {
 #pragma unroll
@@ -137,6 +139,14 @@ __device__ __forceinline__ int wave_bitonic_sort(int v) {
     }
   }
   return v;
+}
+__device__ __forceinline__ int wave_bitonic_sort(int v) { return wave_bitonic_sort(v, lane_id()); }
+
+// The lane id as a value the compiler cannot prove loop-invariant: what is
+// derived from it is recomputed where it is used (see wave_bitonic_sort).
+__device__ __forceinline__ int opaque_lane(int lane) {
+  asm volatile("" : "+v"(lane));
+  return lane;
 }
 
 // ---- several dword ranges set in one launch (dps_scan.hip) ---------------------

@@ -846,6 +846,30 @@ int bank_order(bool p16, int64_t nb, const uint32_t* tile_off, uint32_t* tile_en
   return DPS_OK;
 }
 
+// Count sums per bucket (dps_ct_tiles_sums): 16 lanes per bucket, a sum of
+// the entries' piece values (padding codes add nothing).
+__device__ __forceinline__ uint32_t piece_val(int fmt, uint32_t h) {
+  const uint32_t e = fmt == kFmtU8 ? (h & 7u) : (h & 3u);
+  const uint32_t lab = h >> ent_lsh(fmt);
+  return e > ent_max_e(fmt, lab) ? 0u : (1u << e);
+}
+__global__ __launch_bounds__(kBlock) void k_tile_sums(const uint32_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ ent, int64_t nb,
+                                                      int fmt, uint32_t* __restrict__ sum) {
+  const int sub = threadIdx.x & 15;
+  for (int64_t b = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) >> 4; b < nb;
+       b += (static_cast<int64_t>(gridDim.x) * kBlock) >> 4) {
+    uint32_t s = 0;
+    for (uint32_t i = off[b] + sub; i < off[b + 1]; i += 16) {
+      const uint32_t w = ent[i];
+      s += fmt == kFmt32 ? (w >> 16) : piece_val(fmt, w & 0xFFFFu) + piece_val(fmt, w >> 16);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+    if (sub == 0) sum[b] = s;
+  }
+}
+
 }  // namespace
 }  // namespace dps
 
@@ -905,6 +929,20 @@ size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t ti
   s += align_up(static_cast<size_t>(np + 1) * sizeof(uint32_t));  // part_n
   s += align_up(static_cast<size_t>(n_targets > 0 ? n_targets : 1) * sizeof(int32_t));  // perm
   return s + 1024;
+}
+
+int dps_ct_tiles_sums(const uint32_t* tile_off, const uint32_t* tile_ent, int64_t n_buckets,
+                      int32_t tile_w, uint32_t* tile_sum, void* stream) {
+  DPS_REQUIRE(n_buckets >= 0, DPS_ERR_INVALID, "bad n_buckets");
+  DPS_REQUIRE(tile_w >= 256 && tile_w <= 65536 && (tile_w & (tile_w - 1)) == 0, DPS_ERR_INVALID,
+              "tile_w must be a power of two in [256, 65536]");
+  if (n_buckets == 0) return DPS_OK;
+  DPS_REQUIRE(tile_off && tile_ent && tile_sum, DPS_ERR_INVALID, "null array");
+  const int fmt = tile_fmt(log2_exact(tile_w));
+  k_tile_sums<<<grid_for(n_buckets * 16, kBlock), kBlock, 0, static_cast<hipStream_t>(stream)>>>(
+      tile_off, tile_ent, n_buckets, fmt, tile_sum);
+  DPS_LAUNCHED();
+  return DPS_OK;
 }
 
 int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,

@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPATHSIM_LIB", os.path.join(_HERE, "libdpathsim.so"))
 
-ABI_VERSION = 3  # DPS_ABI_VERSION in include/dpathsim.h
+ABI_VERSION = 4  # DPS_ABI_VERSION in include/dpathsim.h
 
 DPS_OK = 0
 DPS_ERR_INVALID = -1
@@ -35,7 +35,7 @@ class CctExt(C.Structure):
     hv_c, n_hv) and the companion u8 tiles of tile_w 16384 (half_*)."""
     _fields_ = [("s", C.c_void_p), ("hv_slot", C.c_void_p), ("hv_c", C.c_void_p),
                 ("n_hv", C.c_int32), ("half_off", C.c_void_p), ("half_ent", C.c_void_p),
-                ("half_maxc", C.c_void_p)]
+                ("half_maxc", C.c_void_p), ("tile_sum", C.c_void_p)]
 
 _i32 = C.c_int32
 _i64 = C.c_int64
@@ -77,6 +77,7 @@ SIGNATURES = {
     "dps_target_order": (C.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "dps_ct_tiles_workspace_size": (_sz, [_i64, _i64, _i32]),
     "dps_ct_tiles_ent_capacity": (_i64, [_i64, _i64, _i64, _i64, _i32]),
+    "dps_ct_tiles_sums": (C.c_int, [_p, _p, _i64, _i32, _p, _p]),
     "dps_ct_tiles_build": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p,
                                      _p, _sz, _p]),
     "dps_cct_topk_workspace_size": (_sz, []),

@@ -109,6 +109,9 @@ class PathSimEngine:
         self.n_heavy = DEFAULT_HEAVY_VENUES
         # tile_w 16384: the companion 8192-target u8 tiles for wide tiles
         self.half_tiles = True
+        # ... and optimistic 4-bit passes over tiles whose bound is 16..255
+        # (dps_cct_ext.tile_sum; exact either way, fewer passes)
+        self.opt_passes = False   # round 4: measured, see DESIGN §6 (off until it wins)
         self._ext = None
         # symmetric mode (dps_cct_sym): every pair scanned once; whole-range
         # launches at tile_w 8192 / 16384 (venue skipping does not apply there)
@@ -312,7 +315,15 @@ class PathSimEngine:
                           _ptr(t_rank), NA, NV, 8192, _ptr(h_off), _ptr(h_ent), _ptr(h_maxc), None,
                           _ptr(h_status), _ptr(hws), hws.numel(), st)
                 del hws
-                half = (h_off, h_ent, h_maxc, h_status)
+                # per-bucket count sums of the companion tiles: the hot kernel's
+                # optimistic 4-bit passes check each half's digit sum against
+                # them (dps_cct_ext.tile_sum)
+                t_sum = None
+                if self.opt_passes:
+                    t_sum = self._empty(NV * T8, torch.int32)
+                    _lib.call("dps_ct_tiles_sums", _ptr(h_off), _ptr(h_ent), NV * T8, 8192,
+                              _ptr(t_sum), st)
+                half = (h_off, h_ent, h_maxc, h_status, t_sum)
                 mark("half_tiles")
             hv_slot = hv_c = None
             if self.venue_skip and self.denominator == "rowsum" and NA and NV:
@@ -333,6 +344,7 @@ class PathSimEngine:
                  ap_nnz=ap_nnz, px_nnz=px_nnz, sp_status=sp_status, hv_slot=hv_slot, hv_c=hv_c,
                  half_off=half[0] if half else None, half_ent=half[1] if half else None,
                  half_maxc=half[2] if half else None, half_status=half[3] if half else None,
+                 tile_sum=half[4] if half else None,
                  topk_ws=self._ws(_lib.size("dps_cct_topk_workspace_size")))
         self._ext = None
         if hv_c is not None or half is not None:
@@ -340,7 +352,7 @@ class PathSimEngine:
                 _ptr(s) if hv_c is not None else None, _ptr(hv_slot), _ptr(hv_c),
                 min(self.n_heavy, 64) if hv_c is not None else 0,
                 _ptr(half[0]) if half else None, _ptr(half[1]) if half else None,
-                _ptr(half[2]) if half else None)
+                _ptr(half[2]) if half else None, _ptr(half[4]) if half else None)
         self.built = True
         if timed:
             torch.cuda.synchronize(self.device)
@@ -390,12 +402,13 @@ class PathSimEngine:
         return self._dev[name]
 
     def kernel_counts(self):
-        """Work counts of the last W = 8192 hot-kernel launch (its workspace):
+        """Work counts of the last one-wave hot-kernel launch (its workspace):
         rows dequeued, accumulator passes, 16-byte chunks scattered, candidates
-        completed from the heavy-venue table (venue skipping)."""
-        w = self._dev["topk_ws"][:32].view(torch.int64).cpu().tolist()
+        completed from the heavy-venue table (venue skipping), optimistic 4-bit
+        passes that overflowed and ran again as u8 halves."""
+        w = self._dev["topk_ws"][:64].view(torch.int64).cpu().tolist()
         return {"dequeued": int(w[0]), "passes": int(w[1]), "chunks": int(w[2]),
-                "verified": int(w[3])}
+                "verified": int(w[3]), "opt_redo": int(w[4])}
 
     def _ext_arg(self):
         """Host pointer to the dps_cct_ext struct (None = no extension)."""

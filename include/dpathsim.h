@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define DPS_ABI_VERSION 3
+#define DPS_ABI_VERSION 4
 
 enum {
   DPS_OK = 0,
@@ -285,6 +285,12 @@ int dps_target_order(const int64_t* g, int64_t n_targets, int32_t key_bits,
  * inside a bucket is unspecified (results are exact integer sums).
  * ------------------------------------------------------------------------- */
 size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t tile_w);
+/* Per-bucket count sums of built tiles: tile_sum[b] = sum over the bucket's
+ * entries of their values (2^e of a 16-bit piece, padding codes excluded; C of
+ * a 32-bit entry) = sum_{y of tile t} C[y,v] for bucket b = v*T + t, b <
+ * n_buckets = n_mids*T.  uint32 [n_buckets]. */
+int dps_ct_tiles_sums(const uint32_t* tile_off, const uint32_t* tile_ent, int64_t n_buckets,
+                      int32_t tile_w, uint32_t* tile_sum, void* stream);
 /* uint32 words tile_ent must hold for nnz = nnz(C[0:n_targets]) and any
  * sum_c >= the sum of those entries' values (e.g. sum(s)): padding included,
  * plus one spare 16-byte chunk.  0 if sum_c < nnz. */
@@ -340,6 +346,14 @@ typedef struct dps_cct_ext {
   const uint32_t* half_off;
   const uint32_t* half_ent;
   const uint32_t* half_maxc;
+  /* (3) optimistic 4-bit passes (with (1) only; NULL: off): tile_sum = the
+   * per-bucket count sums of the COMPANION u8 tiles (dps_ct_tiles_sums over
+   * half_off / half_ent at 8192).  A 16384-target tile whose bound exceeds 15
+   * (up to 255) then takes ONE 4-bit pass; a count that reached 16 is detected
+   * exactly, per 8192-target half, from the digit sum of that half's counters,
+   * and only such a half runs again as its u8 half tile.  Same results, fewer
+   * accumulator passes. */
+  const uint32_t* tile_sum;
 } dps_cct_ext;
 int dps_heavy_venues(const uint32_t* n_v, int64_t n_mids, int32_t n_hv, int32_t* hv_slot,
                      void* stream);
@@ -430,9 +444,9 @@ int dps_topk_merge(const int32_t* piece_idx, const int64_t* piece_cnt, const dou
  * venue skipping).  Row x in tile a:
  *   1. band pass: x over the tiles [a - band, a + band] (heavy-first order
  *      row_order, may be NULL), its band list into out_*;
- *   2. rows whose band list holds k positive scores ("strong") continue over
- *      the tiles above a + band with the band's k-th score as the threshold;
- *      the others scan every tile.  A pair with y in a tile above a + band is
+ *   2. rest pass, rows in descending label order: rows whose band list holds
+ *      k positive scores ("strong") continue over the tiles above a + band
+ *      with the band's k-th score as the threshold; the others scan every tile.  A pair with y in a tile above a + band is
  *      seen by x alone: it becomes a record (y <- x, M) when its score reaches
  *      y's band k-th score (rounded down to fp32), which bounds y's final k-th
  *      score from below, so no pair of y's top-k is lost;

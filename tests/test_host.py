@@ -25,7 +25,7 @@ def test_header_symbols_exported():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(_lib.exported_symbols()) == declared
-    assert lib.dps_abi_version() == 3
+    assert lib.dps_abi_version() == 4
 
 
 def test_no_cpu_fallback_when_library_missing(monkeypatch):
@@ -184,16 +184,16 @@ def test_c_abi_rejects_bad_arguments_without_gpu():
     # venue skipping: the struct's table width and pointers are validated too
     ws = C.create_string_buffer(512)
     ws_al = (C.addressof(ws) + 255) // 256 * 256
-    vs = _lib.CctExt(1, 1, 1, 65, None, None, None)
+    vs = _lib.CctExt(1, 1, 1, 65, None, None, None, None)
     rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 256, 8, 8, None, 8,
                           C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 256, None)
     assert rc == _lib.DPS_ERR_INVALID and b"n_hv" in lib.dps_last_error()
-    vs = _lib.CctExt(1, None, 1, 32, None, None, None)
+    vs = _lib.CctExt(1, None, 1, 32, None, None, None, None)
     rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 256, 8, 8, None, 8,
                           C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 256, None)
     assert rc == _lib.DPS_ERR_INVALID and b"venue skipping" in lib.dps_last_error()
     # companion u8 tiles belong to tile_w 16384 only
-    vs = _lib.CctExt(None, None, None, 0, 8, 8, 8)
+    vs = _lib.CctExt(None, None, None, 0, 8, 8, 8, None)
     rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 256, 8, 8, None, 8,
                           C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 256, None)
     assert rc == _lib.DPS_ERR_INVALID and b"16384" in lib.dps_last_error()

@@ -46,7 +46,9 @@ for W, NW in cases:
         o = [a.cpu().numpy() for a in o]
         import hashlib
         dig = hashlib.sha1(b"".join(a.tobytes() for a in o)).hexdigest()[:16]
-        print(f"{cfg} W={W} NW={NW}: {best:.2f} ms for {R} rows (k={K}) digest {dig}", flush=True)
+        kc = eng.kernel_counts()
+        print(f"{cfg} W={W} NW={NW}: {best:.2f} ms for {R} rows (k={K}) digest {dig} "
+              f"passes {kc['passes']} chunks {kc['chunks']} redo {kc.get('opt_redo', 0)}", flush=True)
         if ref is None:
             ref = o
         else:

@@ -8,11 +8,10 @@ name=$1; shift
 mkdir -p ../../ab
 src=dps_cct1.hip
 if [ -n "${SRC:-}" ]; then
-  src=/tmp/cct1_src_$name.hip
+  src=build/_cct1_src_$name.hip   # in csrc/build: its includes resolve to csrc/
   git show "$SRC:distributed-pathsim_amd/csrc/dps_cct1.hip" > $src
-  cp dps_cct_dev.hpp dps_common.hpp /tmp/ 2>/dev/null || true
 fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -I. -Wall -Wno-unused-function \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -I. -I.. -Wall -Wno-unused-function \
   -Wno-pass-failed -munsafe-fp-atomics "$@" -c $src -o /tmp/cct1_$name.o
 objs=$(ls build/*.o | grep -v dps_cct1)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../ab/libdpathsim_$name.so /tmp/cct1_$name.o $objs \
