@@ -904,7 +904,10 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
 #ifndef DPS_W5_KPL
 #define DPS_W5_KPL 1
 #endif
-template <int F, int KPL, bool HV, bool SY>
+// OPT: the optimistic 4-bit passes compiled in (launched only with tile_sum:
+// the instantiation without them keeps the old register allocation -- the
+// redo queue and the check alone cost 3 ms of the non-optimistic launch).
+template <int F, int KPL, bool HV, bool SY, bool OPT>
 // The symmetric-mode instantiation carries the record path and the published
 // bounds: DPS_SYM_WPE waves per SIMD (4: 128 VGPRs, no spills).
 #ifndef DPS_SYM_WPE
@@ -997,7 +1000,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       // next stage: the pending half, else the next live tile -- when dual and
       // its 4-bit bound exceeds 15, an optimistic 4-bit pass (opt) or, above
       // kOptMax, its two u8 halves
-      const bool opt_ok = !SY && kOptMax > 0 && dual && p.tile_sum != nullptr && d <= kWave;
+      const bool opt_ok = OPT && !SY && kOptMax > 0 && dual && d <= kWave;
       // the u8 halves of an overflowed opt tile, queued (they run after the
       // prefetched next stage: tiles may be visited in any order)
       // (t8 << 8 | bound, bound <= kOptMax <= 255).  At most four: a check
@@ -1030,7 +1033,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
         uint32_t hbn = 0;
         tn = next_tile<SY>(p, w, t_end, pb, d, c, vT, vT8, dual, lane, tau, gxf, ubn, hbn, ra.far);
         if (!dual || tn < 0 || ubn <= Fmt<F>::UB0) return;
-        if (opt_ok && ubn <= kOptMax) {
+        // (judged in the epilogue, a half's candidates wait in the queue: with
+        // the list not yet full every count is one, so no opt pass then)
+        if (opt_ok && ubn <= kOptMax && (!DPS_OPT_INEPI || tau > 0.0)) {
           optn = true;
           hbo = hbn;
           return;
@@ -1136,7 +1141,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
             // next stage's first chunks are in flight during the check
             // (S_hb != 0 for an opt stage: its bound exceeds 15, so one half's
             // bound is positive; S_exp: the two halves' expected sums, 16 bits each)
-            const uint32_t S_hb = X.opt ? X.hb : 0u;
+            const uint32_t S_hb = OPT && X.opt ? X.hb : 0u;
             const uint32_t S_exp = X.exp;
             if (prof) ts[2] = __builtin_amdgcn_s_memtime();
             if (last) {
@@ -1188,6 +1193,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
             if (S_hb != 0u) {
 #ifdef DPS_EXP_NOCHECK
               bmask = 0xFFu;       // experiment only: wrong results when a count overflows
+#elif defined(DPS_EXP_CHECKONLY)
+              {                    // experiment only: the check runs, its result is ignored
+                const uint32_t bm = opt_check(acc, S_exp, lane);
+                asm volatile("" ::"s"(bm));
+              }
 #else
               bmask = opt_check(acc, S_exp, lane);
 #endif
@@ -1207,7 +1217,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
             } else {
               epi1_wide<F, KPL, HV, SY>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, ra);
             }
-            if (bad) {
+            if (OPT && bad) {
               // halves of an optimistic pass with a count that reached 16: run
               // again as their u8 half tiles, queued for a later stage (half
               // bounds <= the opt tile's bound <= kOptMax: never saturated)
@@ -1317,9 +1327,12 @@ int launch1(const CctParams& p, hipStream_t st) {
 #endif
   int64_t grid = static_cast<int64_t>(n_cu) * wpc;
   if (grid > p.n_rows) grid = p.n_rows;
-  if (p.sym) k_cct1<F, KPL, false, true><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
-  else if (p.hv_c) k_cct1<F, KPL, true, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
-  else k_cct1<F, KPL, false, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  const bool opt = F == 2 && p.tile_sum != nullptr && p.h_ent != nullptr && kOptMax > 0;
+  if (p.sym) k_cct1<F, KPL, false, true, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  else if (p.hv_c && opt) k_cct1<F, KPL, true, false, true><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  else if (p.hv_c) k_cct1<F, KPL, true, false, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  else if (opt) k_cct1<F, KPL, false, false, true><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  else k_cct1<F, KPL, false, false, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
   DPS_LAUNCHED();
   return DPS_OK;
 }

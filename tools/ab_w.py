@@ -29,6 +29,9 @@ for W, NW in cases:
         eng = PathSimEngine(t, tile_w=W)
         if os.environ.get("AB_NHEAVY"):
             eng.n_heavy = int(os.environ["AB_NHEAVY"])
+        # optimistic 4-bit passes (engine.opt_passes, dps_cct_ext.tile_sum): on in
+        # A/B runs unless AB_OPT=0 (a library without them ignores tile_sum)
+        eng.opt_passes = os.environ.get("AB_OPT", "1") == "1"
         eng.upload().build()
         W0 = W
         eng.build(timed=True)

@@ -43,6 +43,9 @@ row_of = np.repeat(np.arange(NA), np.diff(cp))
 tl = rank // W
 maxc = np.zeros((NV, T), np.int64)
 np.maximum.at(maxc, (cc, tl[row_of]), cv)
+T8 = (NA + W // 2 - 1) // (W // 2)
+maxh = np.zeros((NV, T8), np.int64)
+np.maximum.at(maxh, (cc, (rank // (W // 2))[row_of]), cv)
 n_v = np.bincount(cc, minlength=NV)
 deg = np.diff(cp)
 terms = np.add.reduceat(n_v[cc], cp[:-1]) * (deg > 0)
@@ -51,7 +54,7 @@ qs = np.quantile(terms, [0, 0.33, 0.66, 0.9, 1.0])
 for band in range(4):
     pool = np.flatnonzero((terms >= qs[band]) & (terms <= qs[band + 1]) & (deg > 0))
     rows = rng.choice(pool, min(nrows, len(pool)), replace=False)
-    live = split = ovf = ovf_h = 0
+    live = split = ovf = ovf_h = both15 = chk_h = 0
     n = 0
     for x in rows:
         a0, a1 = cp[x], cp[x + 1]
@@ -71,10 +74,16 @@ for band in range(4):
         mh = np.zeros(2 * T, np.int64)
         np.maximum.at(mh, rank // (W // 2), mrow)
         sp_t = lv & (ub > 15)
+        uh = (a[:, None] * maxh[v]).sum(0)
+        uh = np.pad(uh, (0, 2 * T - len(uh)))
+        ha, hb2 = uh[0::2], uh[1::2]
+        both15 += (sp_t & (ha <= 15) & (hb2 <= 15)).sum()
+        chk_h += (sp_t & (ha > 15)).sum() + (sp_t & (hb2 > 15)).sum()
         live += lv.sum()
         split += sp_t.sum()
         ovf += (sp_t & (mt >= 16)).sum()
         ovf_h += (np.repeat(sp_t, 2)[: len(mh)] & (mh >= 16)).sum()
     print(f"{cfg} band {band} (row work {qs[band]:.0f}..{qs[band + 1]:.0f}), {n} rows: live tiles/row "
           f"{live / n:.1f}, bound > 15: {split / n:.1f}, of which a count >= 16: {ovf / n:.2f} tiles "
-          f"({ovf_h / n:.2f} halves)", flush=True)
+          f"({ovf_h / n:.2f} halves); both half bounds <= 15: {both15 / n:.1f} tiles; halves with a "
+          f"bound > 15 (to check): {chk_h / n:.1f}", flush=True)
