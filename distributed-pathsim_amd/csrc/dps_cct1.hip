@@ -61,6 +61,21 @@ namespace {
 // when the caller provides one ("dual", p.h_ent): each half scatters only its
 // own entries, through the same branch-free path; without it the tile takes
 // wide 4-bit passes (u8 / u16 / u32 counters, one entry at a time).
+// A kernel parameter read where it is used -- an s_load from the kernarg
+// segment each time (the kernel's only argument is the CctParams, at offset
+// 0) -- instead of being held in SGPRs, or spilled to VGPR lanes, across the
+// whole row loop: for the fields only the per-row code needs.  The asm
+// launders the base so the loads cannot be hoisted back out of the loop.
+// (Taking p's address instead would copy the struct to scratch.)
+template <class T>
+__device__ __forceinline__ T kcold_at(size_t off) {
+  typedef const __attribute__((address_space(4))) char* kb;
+  kb base = (kb)(__builtin_amdgcn_kernarg_segment_ptr());
+  asm volatile("" : "+s"(base));
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(base + off);
+}
+#define kcold(field) kcold_at<decltype(CctParams::field)>(offsetof(CctParams, field))
+
 constexpr int kAcc1 = 2048;                   // accumulator dwords (8 KiB)
 constexpr uint32_t kLabMask1 = 0x1FFCu;       // (entry >> 3) & mask = dword byte address
 template <int F> struct Fmt;
@@ -123,20 +138,6 @@ __device__ __forceinline__ void zero_trip(uint32_t* acc, int b0, int lane) {
     *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
 }
 
-// A kernel parameter read where it is used -- an s_load from the kernarg
-// segment each time (the kernel's only argument is the CctParams, at offset
-// 0) -- instead of being held in SGPRs, or spilled to VGPR lanes, across the
-// whole row loop: for the fields only the per-row code needs.  The asm
-// launders the base so the loads cannot be hoisted back out of the loop.
-// (Taking p's address instead would copy the struct to scratch.)
-template <class T>
-__device__ __forceinline__ T kcold_at(size_t off) {
-  typedef const __attribute__((address_space(4))) char* kb;
-  kb base = (kb)(__builtin_amdgcn_kernarg_segment_ptr());
-  asm volatile("" : "+s"(base));
-  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(base + off);
-}
-#define kcold(field) kcold_at<decltype(CctParams::field)>(offsetof(CctParams, field))
 
 // Symmetric rest pass: the bounds other rows raise are read with plain loads
 // (any value read is a valid bound; an atomic load would wait for every
@@ -158,7 +159,8 @@ struct Win1 {
   float gmf;       // lane: smallest g of the tile, as float
   uint64_t live;   // tiles not yet visited that may hold a top-k target
   uint64_t ykeep;  // symmetric rest pass: tiles that may hold a pair to hand on
-  double tau;      // tau the mask was last filtered with
+  float tau;       // tau the mask was last filtered with (rounded: a missed tiny rise
+                   // only postpones a refilter)
 };
 constexpr uint32_t kHalfSat = 0xFFFFu;
 
@@ -184,8 +186,8 @@ __device__ __forceinline__ uint32_t win_ub(const CctParams& p, int w0, int t_end
     uint32_t vg = vT, vg8 = vT8;
     if (g0 > 0) {
       const int j = g0 + lane;
-      cg = j < d ? p.c_val[pb + j] : 0;
-      const uint32_t vj = j < d ? static_cast<uint32_t>(p.c_col[pb + j]) : 0u;
+      cg = j < d ? kcold(c_val)[pb + j] : 0;
+      const uint32_t vj = j < d ? static_cast<uint32_t>(kcold(c_col)[pb + j]) : 0u;
       vg = vj * static_cast<uint32_t>(p.T);
       vg8 = dual ? vj * static_cast<uint32_t>(p.T8) : 0u;
     }
@@ -237,7 +239,7 @@ __device__ __forceinline__ void win_load(const CctParams& p, Win1& w, int w0, in
                      w.ub >= static_cast<uint32_t>(max(mneed_lo32(ty, gxf + w.gmf), 1)));
   }
   w.live = ballot(t >= t_lo && t < t_end && w.ub > 0) & (win_pass(w, tau, gxf) | w.ykeep);
-  w.tau = tau;
+  w.tau = static_cast<float>(tau);
 }
 
 // Next tile to process (-1: none left); slides the window as needed.
@@ -577,7 +579,7 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
   const int tpd_shift = (F == 1 ? 2 : 3) - lnp;      // log2(targets per dword)
   const uint32_t vmask = bits == 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
   const int blnp = bits == 8 ? 0 : bits == 16 ? 1 : 2;   // block_any's counter width
-  const int64_t tile_base = S.t << kS1;
+  const int64_t tile_base = static_cast<int64_t>(S.t) << kS1;
   const int pass_base = S.pass << (kS1 - lnp);
   for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4) {
     const int b = b0 + lane * 4;
@@ -881,10 +883,10 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
     uint32_t lo = 0, hi = 0;
     int c = 0;
     if (j < d) {
-      const uint32_t b = static_cast<uint32_t>(p.c_col[pb + j]) * T + static_cast<uint32_t>(S.t);
+      const uint32_t b = static_cast<uint32_t>(kcold(c_col)[pb + j]) * T + static_cast<uint32_t>(S.t);
       lo = off[b];
       hi = off[b + 1];
-      c = p.c_val[pb + j];
+      c = kcold(c_val)[pb + j];
     }
     Stage E = S;
     grp_set(E.G, lo, hi, c, d - g0 < kWave ? d - g0 : kWave);
@@ -939,24 +941,23 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
   for (;;) {
     unsigned long long rr = 0;
     if (lane == 0) rr = atomicAdd(kcold(counter), 1ull);
-    const int64_t r = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rr)));
+    const int r = __builtin_amdgcn_readfirstlane(static_cast<int>(rr));
     if (r >= kcold(n_rows)) break;
     const int32_t* row_order = kcold(row_order);
-    const int64_t x = row_order ? static_cast<int64_t>(row_order[r]) : kcold(row_begin) + r;
+    const int x = row_order ? row_order[r] : static_cast<int>(kcold(row_begin) + r);   // < 2^31
     const bool is_piece = r < kcold(n_pieces);
-    const int64_t ro = (is_piece || kcold(out_by_slot)) ? r : x - kcold(row_begin);
     int t_beg = is_piece ? kcold(piece_t0)[r] : 0;
     int t_end = is_piece ? kcold(piece_t1)[r] : static_cast<int>(p.T);
     DPS_DASSERT(0 <= t_beg && t_beg <= t_end && t_end <= p.T);
     const int32_t* t_rank = kcold(t_rank);
-    const int64_t x_lab = t_rank ? static_cast<int64_t>(t_rank[x]) : x;
+    const int x_lab = t_rank ? t_rank[x] : static_cast<int>(x);   // labels < 2^31
     const int64_t* c_ptr = kcold(c_ptr);
     const int64_t pb = c_ptr[x];
     const int d = static_cast<int>(c_ptr[x + 1] - pb);
     const int64_t gx = kcold(g)[x];
     const float gxf = i64_f32(gx);
     TopK<KPL> top;
-    top.init(p.k);
+    top.init(kcold(k));
     ra.x = static_cast<int>(x);
     ra.far = INT_MAX;
     bool strong = false;                // sym rest pass: a partial list, no zero fill
@@ -969,7 +970,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
         ra.far = a + p.band + 1;
         strong = p.row_strong[x] != 0;
         if (strong) {                   // tiles above the band, its k-th as the floor
-          const int64_t e = x * p.k + p.k - 1;
+          const int64_t e = static_cast<int64_t>(x) * p.k + p.k - 1;
           top.set_floor(p.seed_score[e], p.seed_idx[e]);
           t_beg = max(t_beg, ra.far);
         }
@@ -1149,9 +1150,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
               // chunks in flight, then load the bounds of the one after
               bool row_done = false;
               hchg = false;
-              if (tau > w.tau) {
+              if (static_cast<float>(tau) > w.tau) {
                 w.live &= win_pass(w, tau, gxf) | w.ykeep;
-                w.tau = tau;
+                w.tau = static_cast<float>(tau);
                 if (HV) {
                   // H = the heavy venues with C[x,h] / s_h <= tau / 2 (hr is an
                   // upper bound of the ratio, th a lower bound of tau / 2); with
@@ -1262,6 +1263,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
 
     // ranked entries, then zero-score targets in reference order, then -1
     const int kk = kcold(k);
+    const int64_t ro = (is_piece || kcold(out_by_slot)) ? r : x - kcold(row_begin);
     int32_t* oi = (is_piece ? kcold(piece_idx) : kcold(out_idx)) + ro * kk;
     int64_t* oc = (is_piece ? kcold(piece_cnt) : kcold(out_cnt)) + ro * kk;
     double* os = (is_piece ? kcold(piece_score) : kcold(out_score)) + ro * kk;
@@ -1271,7 +1273,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       if (slot < top.filled) { oi[slot] = top.y[q]; oc[slot] = top.m[q]; os[slot] = top.s[q]; }
     }
     const int64_t avail = p.n_targets - 1;
-    const int want = (is_piece || strong) ? top.filled : static_cast<int>(avail < p.k ? avail : p.k);
+    const int want = (is_piece || strong) ? top.filled : static_cast<int>(avail < kk ? avail : kk);
     int slot = top.filled;
     for (int64_t yb = 0; slot < want && yb < p.n_targets; yb += kWave) {
       const int64_t yc = yb + lane;
@@ -1291,7 +1293,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       }
       slot += __popcll(mk);
     }
-    for (int s2 = want + lane; s2 < p.k; s2 += kWave) {
+    for (int s2 = want + lane; s2 < kk; s2 += kWave) {
       oi[s2] = -1;
       oc[s2] = 0;
       os[s2] = 0.0;
@@ -1299,10 +1301,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
     if (SY && p.sym == 2) sym_publish<KPL>(p, x_lab, strong, top, lane);
   }
   if (lane == 0 && (n_pass | n_chunk)) {
-    atomicAdd(p.counter + 1, static_cast<unsigned long long>(n_pass));
-    atomicAdd(p.counter + 2, static_cast<unsigned long long>(n_chunk));
-    if (HV && ra.ver) atomicAdd(p.counter + 3, static_cast<unsigned long long>(ra.ver));
-    if (ra.redo) atomicAdd(p.counter + 4, static_cast<unsigned long long>(ra.redo));
+    unsigned long long* ctr = kcold(counter);
+    atomicAdd(ctr + 1, static_cast<unsigned long long>(n_pass));
+    atomicAdd(ctr + 2, static_cast<unsigned long long>(n_chunk));
+    if (HV && ra.ver) atomicAdd(ctr + 3, static_cast<unsigned long long>(ra.ver));
+    if (ra.redo) atomicAdd(ctr + 4, static_cast<unsigned long long>(ra.redo));
   }
   if (prof && lane == 0) {
 #pragma unroll

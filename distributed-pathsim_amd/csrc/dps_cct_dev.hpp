@@ -306,7 +306,7 @@ __device__ __forceinline__ int chunk_venue(const Grp& G, const int (&sp)[kSmallG
 // the tile, so no lane can carry into its neighbour.
 struct Stage {
   Grp G;
-  int64_t t;
+  int t;         // tile (< 2^31: tile offsets are 32-bit)
   int lnp;       // log2(number of passes): 0 u8, 1 u16, 2 u32
   int pass;
   int nb;        // batches of NW*64*kU chunks (0 under the no-scatter ablation)
@@ -585,7 +585,7 @@ __device__ __forceinline__ void epilogue_u8(const CctParams& p, uint32_t* acc, T
                                             double tau_sh, int mseg) {
   const int qd = nbuf / NW;
   const int end = (wave + 1) * qd;
-  const int64_t tile_base = S.t << p.shift;
+  const int64_t tile_base = static_cast<int64_t>(S.t) << p.shift;
   const bool score = !kProfile || (p.ablate & 2) == 0;
   const int64_t xr64 = x_lab - tile_base;
   const int xrel = (xr64 >= 0 && xr64 < (int64_t(1) << p.shift)) ? static_cast<int>(xr64) : -64;
@@ -690,7 +690,7 @@ __device__ __forceinline__ void epilogue(const CctParams& p, uint32_t* acc, TopK
   const int tpd_shift = 2 - lnp;                     // log2(targets per dword)
   const int bits = 8 << lnp;
   const uint32_t vmask = lnp == 2 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
-  const int64_t tile_base = S.t << p.shift;
+  const int64_t tile_base = static_cast<int64_t>(S.t) << p.shift;
   const int pass_base = S.pass << (p.shift - lnp);
   const bool score = !kProfile || (p.ablate & 2) == 0;
   for (int b0 = wave * qd; b0 < end; b0 += kWave * 4) {
