@@ -820,9 +820,12 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
 // base and C.  Boundaries inside a load are resolved without LDS round trips:
 // up to kSel of them by a per-boundary select over readlane'd scalars, more by
 // counting the boundaries each lane has passed and fetching base and C from
-// that venue's lane with two independent bpermutes.
+// that venue's lane with two independent bpermutes.  (kSel swept on the full
+// config3 launch: 4 / 8 / 16 = 72.3 / 73.2 / 73.8 ms in round 3; with the
+// round-4 register allocation 1 / 2 / 3 / 4 / 6 = 66.45 / 66.5 / 66.65 / 66.86
+// / 67.3 ms, profiles/r04/ab/ab4n, ab4o.)
 #ifndef DPS_KSEL
-#define DPS_KSEL 4
+#define DPS_KSEL 2
 #endif
 constexpr int kSel = DPS_KSEL;
 
