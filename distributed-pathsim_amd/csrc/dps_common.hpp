@@ -130,7 +130,9 @@ __device__ __forceinline__ int wave_bitonic_sort(int v, int lane) {
   for (int k = 2; k <= kWave; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      int o = __shfl_xor(v, j, kWave);
+      // partner lane's value by ds_bpermute from `lane` (not __shfl_xor, whose
+      // lane-constant addresses the compiler would also hoist)
+      int o = __builtin_amdgcn_ds_bpermute((lane ^ j) << 2, v);
       bool up = (lane & k) == 0;
       bool lower = (lane & j) == 0;
       int mn = o < v ? o : v;
