@@ -32,6 +32,8 @@ for W, NW in cases:
         # optimistic 4-bit passes (engine.opt_passes, dps_cct_ext.tile_sum): on in
         # A/B runs unless AB_OPT=0 (a library without them ignores tile_sum)
         eng.opt_passes = os.environ.get("AB_OPT", "1") == "1"
+        if os.environ.get("AB_SPLIT"):      # "rows:pieces" of the heavy-row split
+            eng.split_rows, eng.pieces = (int(v) for v in os.environ["AB_SPLIT"].split(":"))
         eng.upload().build()
         W0 = W
         eng.build(timed=True)
