@@ -870,6 +870,129 @@ __global__ __launch_bounds__(kBlock) void k_tile_sums(const uint32_t* __restrict
   }
 }
 
+// --------------------------------------------------------------------------
+// Sorted tile build (dps_ct_tiles_build2, many mids -- config4's 200k topics,
+// where the per-entry global atomics on n_mids * T bucket counters cost 5.8
+// ms): every C entry becomes a (bucket, (local label << 16) | C) pair, one
+// stable LSD radix sort orders them by bucket, and the buckets are then
+// counted, laid out and written from the sorted order -- coalesced, no
+// atomics on the 24.6 M counters.  Pairs past nnz (the capacity is a host
+// bound) carry the key nb and sort last.
+__global__ __launch_bounds__(kBlock) void k_tile_keys(const int64_t* __restrict__ c_ptr,
+                                                      const int32_t* __restrict__ c_col,
+                                                      const int32_t* __restrict__ c_val,
+                                                      const int32_t* __restrict__ rank,
+                                                      const int64_t* __restrict__ g,
+                                                      int64_t n_rows, int shift, int64_t T,
+                                                      uint64_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ vals,
+                                                      unsigned long long* __restrict__ gmin,
+                                                      int32_t* __restrict__ status) {
+  __shared__ unsigned long long gmin_s[kTileGminLds];
+  const bool lds_gmin = gmin && T <= kTileGminLds;
+  if (lds_gmin)
+    for (int64_t i = threadIdx.x; i < T; i += kBlock) gmin_s[i] = ~0ull;
+  __syncthreads();
+  const int lane = lane_id();
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  const uint32_t ymask = (1u << shift) - 1u;
+  for (int64_t y = wave0; y < n_rows; y += nwaves) {
+    const int64_t lab = label_of(rank, y);
+    const int64_t t = lab >> shift;
+    if (lane == 0 && gmin) {
+      if (lds_gmin) atomicMin(&gmin_s[t], static_cast<unsigned long long>(g[y]));
+      else atomicMin(&gmin[t], static_cast<unsigned long long>(g[y]));
+    }
+    const uint32_t l = static_cast<uint32_t>(lab) & ymask;
+    for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
+      int32_t c = c_val[j];
+      if (c > 0xFFFF) {
+        if (status) *status = DPS_ERR_OVERFLOW;
+        c = 0xFFFF;
+      }
+      keys[j] = static_cast<uint64_t>(static_cast<int64_t>(c_col[j]) * T + t);
+      vals[j] = (l << 16) | static_cast<uint32_t>(c);
+    }
+  }
+  __syncthreads();
+  if (lds_gmin)
+    for (int64_t i = threadIdx.x; i < T; i += kBlock)
+      if (gmin_s[i] != ~0ull) atomicMin(&gmin[i], gmin_s[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_tile_keys_pad(const int64_t* __restrict__ c_ptr,
+                                                          int64_t n_rows, int64_t cap, uint64_t nb,
+                                                          uint64_t* __restrict__ keys,
+                                                          uint32_t* __restrict__ vals) {
+  const int64_t nnz = c_ptr[n_rows] - c_ptr[0];
+  for (int64_t i = nnz + static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < cap;
+       i += static_cast<int64_t>(gridDim.x) * kBlock) {
+    keys[i] = nb;
+    vals[i] = 0;
+  }
+}
+
+// Per sorted pair: its pieces (0 past nnz), the first / one-past-last index of
+// its bucket's run (bstart / bend), the bucket maximum (C > 1 only: k_round4
+// style, the counts pass raises a non-empty bucket's maximum to 1).
+__global__ __launch_bounds__(kBlock) void k_sorted_runs(const uint64_t* __restrict__ keys,
+                                                        const uint32_t* __restrict__ vals,
+                                                        int64_t cap, uint64_t nb, int fmt,
+                                                        uint32_t* __restrict__ pieces,
+                                                        uint32_t* __restrict__ bstart,
+                                                        uint32_t* __restrict__ bend,
+                                                        uint32_t* __restrict__ maxc) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < cap;
+       i += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const uint64_t b = keys[i];
+    if (b >= nb) {
+      pieces[i] = 0;
+      continue;
+    }
+    const uint32_t v = vals[i];
+    const uint32_t c = v & 0xFFFFu, l = v >> 16;
+    pieces[i] = n_pieces(fmt, c, l);
+    if (i == 0 || keys[i - 1] != b) bstart[b] = static_cast<uint32_t>(i);
+    if (i + 1 == cap || keys[i + 1] != b) bend[b] = static_cast<uint32_t>(i + 1);
+    if (maxc && c > 1) atomicMax(&maxc[b], c);
+  }
+}
+
+// Bucket b: real pieces (kept in real[] for the padding pass) and the padded
+// count (cnt[], scanned into the layout).
+__global__ __launch_bounds__(kBlock) void k_sorted_counts(const uint32_t* __restrict__ bstart,
+                                                          const uint32_t* __restrict__ bend,
+                                                          const int64_t* __restrict__ P, int64_t nb,
+                                                          uint32_t per16, uint32_t* __restrict__ cnt,
+                                                          uint32_t* __restrict__ real,
+                                                          uint32_t* __restrict__ maxc) {
+  for (int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; b < nb;
+       b += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const uint32_t s0 = bstart[b], s1 = bend[b];
+    const uint32_t n = s1 > s0 ? static_cast<uint32_t>(P[s1] - P[s0]) : 0u;
+    real[b] = n;
+    cnt[b] = padded_count(n, per16);
+    if (maxc && n > 0 && maxc[b] == 0) maxc[b] = 1;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sorted_write(const uint64_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ vals,
+                                                         int64_t cap, uint64_t nb, int fmt,
+                                                         const int64_t* __restrict__ P,
+                                                         const uint32_t* __restrict__ bstart,
+                                                         const int64_t* __restrict__ off,
+                                                         uint32_t* __restrict__ ent) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < cap;
+       i += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const uint64_t b = keys[i];
+    if (b >= nb) continue;
+    const uint32_t v = vals[i];
+    put_entry(fmt, ent, off[b] + (P[i] - P[bstart[b]]), v & 0xFFFFu, v >> 16);
+  }
+}
+
 }  // namespace
 }  // namespace dps
 
@@ -1076,6 +1199,115 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     DPS_LAUNCHED();
   }
   return bank_order(p16, nb, tile_off, tile_ent, st);
+}
+
+size_t dps_ct_tiles_workspace_size2(int64_t n_mids, int64_t n_targets, int32_t tile_w,
+                                    int64_t nnz_cap) {
+  const size_t base = dps_ct_tiles_workspace_size(n_mids, n_targets, tile_w);
+  if (tile_w <= 0 || !tile_global(n_mids)) return base;
+  const int64_t T = (n_targets + tile_w - 1) / tile_w;
+  const size_t nb = static_cast<size_t>(n_mids * (T > 0 ? T : 1));
+  const size_t cap = static_cast<size_t>(nnz_cap > 0 ? nnz_cap : 1);
+  size_t s = 0;
+  s += 2 * align_up(cap * sizeof(uint64_t));          // keys, sorted keys
+  s += 2 * align_up(cap * sizeof(uint32_t));          // vals, sorted vals
+  s += align_up(cap * sizeof(uint32_t));              // pieces
+  s += align_up((cap + 1) * sizeof(int64_t));         // P
+  s += align_up(scan_workspace_size(static_cast<int64_t>(cap)));
+  s += 2 * align_up((nb + 1) * sizeof(uint32_t));     // bstart, bend
+  s += align_up(radix_sort_workspace_size(static_cast<int64_t>(cap)));
+  return base + s + 1024;
+}
+
+int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                        const int64_t* g, const int32_t* t_rank, int64_t n_targets, int64_t n_mids,
+                        int32_t tile_w, int64_t nnz_cap, uint32_t* tile_off, uint32_t* tile_ent,
+                        uint32_t* tile_maxc, int64_t* tile_gmin, int32_t* status_dev, void* ws,
+                        size_t ws_bytes, void* stream) {
+  if (!tile_global(n_mids))
+    return dps_ct_tiles_build(c_ptr, c_col, c_val, g, t_rank, n_targets, n_mids, tile_w, tile_off,
+                              tile_ent, tile_maxc, tile_gmin, status_dev, ws, ws_bytes, stream);
+  const int shift = log2_exact(tile_w);
+  DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED,
+              "tile_w must be a power of two in [256, 65536], got %d", tile_w);
+  DPS_REQUIRE(n_targets >= 0 && n_mids >= 0 && nnz_cap >= 0, DPS_ERR_INVALID, "negative size");
+  DPS_REQUIRE(n_targets < INT32_MAX && nnz_cap < UINT32_MAX, DPS_ERR_OVERFLOW,
+              "n_targets / nnz capacity exceed 32 bits");
+  DPS_REQUIRE(!tile_gmin || g, DPS_ERR_INVALID, "tile_gmin needs g");
+  DPS_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 256 == 0, DPS_ERR_WORKSPACE,
+              "workspace not 256-byte aligned");
+  DPS_REQUIRE(ws_bytes >= dps_ct_tiles_workspace_size2(n_mids, n_targets, tile_w, nnz_cap),
+              DPS_ERR_WORKSPACE, "tiles workspace too small");
+  auto st = static_cast<hipStream_t>(stream);
+  const int64_t T = (n_targets + tile_w - 1) / tile_w;
+  const int64_t nb = n_mids * T;
+  const int64_t cap = nnz_cap > 0 ? nnz_cap : 1;
+  Carve c(ws, ws_bytes);
+  uint32_t* cnt = c.take<uint32_t>(nb + 1);
+  uint32_t* real = c.take<uint32_t>(nb + 1);
+  int64_t* off64 = c.take<int64_t>(nb + 1);
+  const size_t scan_b = scan_workspace_size(nb + 1);
+  void* sws_b = c.take<char>(scan_b);
+  uint64_t* keys = c.take<uint64_t>(cap);
+  uint64_t* keys_s = c.take<uint64_t>(cap);
+  uint32_t* vals = c.take<uint32_t>(cap);
+  uint32_t* vals_s = c.take<uint32_t>(cap);
+  uint32_t* pieces = c.take<uint32_t>(cap);
+  int64_t* P = c.take<int64_t>(cap + 1);
+  const size_t scan_e = scan_workspace_size(cap);
+  void* sws_e = c.take<char>(scan_e);
+  uint32_t* bstart = c.take<uint32_t>(nb + 1);
+  uint32_t* bend = c.take<uint32_t>(nb + 1);
+  const size_t rs_bytes = radix_sort_workspace_size(cap);
+  void* rws = c.take<char>(rs_bytes);
+  DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "tiles workspace carve failed");
+  const int fmt = tile_fmt(shift);
+  const uint32_t per16 = fmt != kFmt32 ? 8u : 4u;
+  {
+    FillSet fs;
+    fs.add(bstart, nb + 1, 0u);
+    fs.add(bend, nb + 1, 0u);
+    if (status_dev) fs.add(status_dev, 1, 0u);
+    if (tile_gmin && T > 0) fs.add(tile_gmin, 2 * T, 0x7F7F7F7Fu);
+    if (tile_maxc) fs.add(tile_maxc, nb + 1, 0u);
+    DPS_HIP_RET(fill_set(fs, st));
+  }
+  if (n_targets > 0) {
+    k_tile_keys<<<grid_for(n_targets * kWave, kBlock, 2048), kBlock, 0, st>>>(
+        c_ptr, c_col, c_val, t_rank, g, n_targets, shift, T, keys, vals,
+        reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
+    DPS_LAUNCHED();
+  }
+  k_tile_keys_pad<<<grid_for(cap, kBlock), kBlock, 0, st>>>(c_ptr, n_targets, cap,
+                                                           static_cast<uint64_t>(nb), keys, vals);
+  DPS_LAUNCHED();
+  int key_bits = 1;
+  while ((int64_t(1) << key_bits) <= nb) ++key_bits;     // nb itself is the pad key
+  DPS_HIP_RET(radix_sort_pairs(keys, vals, keys_s, vals_s, cap, key_bits, rws, rs_bytes, st));
+  k_sorted_runs<<<grid_for(cap, kBlock), kBlock, 0, st>>>(keys_s, vals_s, cap,
+                                                         static_cast<uint64_t>(nb), fmt, pieces,
+                                                         bstart, bend, tile_maxc);
+  DPS_LAUNCHED();
+  DPS_HIP_RET(scan_exclusive<uint32_t>(pieces, P, cap, sws_e, scan_e, st));
+  if (nb > 0) {
+    k_sorted_counts<<<grid_for(nb, kBlock), kBlock, 0, st>>>(bstart, bend, P, nb, per16, cnt, real,
+                                                            tile_maxc);
+    DPS_LAUNCHED();
+  }
+  DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, off64, nb, sws_b, scan_b, st));
+  k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, 1, nb, fmt != kFmt32 ? 1 : 0,
+                                                           tile_off);
+  DPS_LAUNCHED();
+  k_sorted_write<<<grid_for(cap, kBlock), kBlock, 0, st>>>(keys_s, vals_s, cap,
+                                                          static_cast<uint64_t>(nb), fmt, P, bstart,
+                                                          off64, tile_ent);
+  DPS_LAUNCHED();
+  if (nb > 0) {
+    k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(
+        off64, 1, real, nb, static_cast<uint32_t>(tile_w) - 1u, fmt, tile_ent);
+    DPS_LAUNCHED();
+  }
+  return bank_order(fmt != kFmt32, nb, tile_off, tile_ent, st);
 }
 
 int dps_walk_row(const int32_t* src_col, const int32_t* src_val, int64_t src_len,

@@ -78,6 +78,9 @@ SIGNATURES = {
     "dps_ct_tiles_workspace_size": (_sz, [_i64, _i64, _i32]),
     "dps_ct_tiles_ent_capacity": (_i64, [_i64, _i64, _i64, _i64, _i32]),
     "dps_ct_tiles_sums": (C.c_int, [_p, _p, _i64, _i32, _p, _p]),
+    "dps_ct_tiles_workspace_size2": (_sz, [_i64, _i64, _i32, _i64]),
+    "dps_ct_tiles_build2": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _i32, _i64, _p, _p, _p, _p,
+                                      _p, _p, _sz, _p]),
     "dps_ct_tiles_build": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p,
                                      _p, _sz, _p]),
     "dps_cct_topk_workspace_size": (_sz, []),

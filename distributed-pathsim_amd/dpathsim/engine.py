@@ -294,9 +294,11 @@ class PathSimEngine:
                 raise OverflowError("padded nnz(C) >= 2^32 exceeds the uint32 tile offsets")
             tile_ent = self._empty(ent_cap, torch.int32)
             status = self._empty(1, torch.int32)
-            tws = self._ws(_lib.size("dps_ct_tiles_workspace_size", NV, NA, self.tile_w))
-            _lib.call("dps_ct_tiles_build", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(den),
-                      _ptr(t_rank), NA, NV, self.tile_w, _ptr(tile_off), _ptr(tile_ent),
+            # (many mids: laid out from one radix sort of (bucket, entry) pairs,
+            # dps_ct_tiles_build2; bnd.expand bounds nnz over the author rows)
+            tws = self._ws(_lib.size("dps_ct_tiles_workspace_size2", NV, NA, self.tile_w, bnd.expand))
+            _lib.call("dps_ct_tiles_build2", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(den),
+                      _ptr(t_rank), NA, NV, self.tile_w, bnd.expand, _ptr(tile_off), _ptr(tile_ent),
                       _ptr(tile_maxc), _ptr(tile_gmin), _ptr(status), _ptr(tws), tws.numel(), st)
             mark("tiles")
             del tws
@@ -310,10 +312,10 @@ class PathSimEngine:
                 h_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV, NA, 8192)
                 h_ent = self._empty(h_cap, torch.int32)
                 h_status = self._empty(1, torch.int32)
-                hws = self._ws(_lib.size("dps_ct_tiles_workspace_size", NV, NA, 8192))
-                _lib.call("dps_ct_tiles_build", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), None,
-                          _ptr(t_rank), NA, NV, 8192, _ptr(h_off), _ptr(h_ent), _ptr(h_maxc), None,
-                          _ptr(h_status), _ptr(hws), hws.numel(), st)
+                hws = self._ws(_lib.size("dps_ct_tiles_workspace_size2", NV, NA, 8192, bnd.expand))
+                _lib.call("dps_ct_tiles_build2", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), None,
+                          _ptr(t_rank), NA, NV, 8192, bnd.expand, _ptr(h_off), _ptr(h_ent),
+                          _ptr(h_maxc), None, _ptr(h_status), _ptr(hws), hws.numel(), st)
                 del hws
                 # per-bucket count sums of the companion tiles: the hot kernel's
                 # optimistic 4-bit passes check each half's digit sum against

@@ -285,6 +285,19 @@ int dps_target_order(const int64_t* g, int64_t n_targets, int32_t key_bits,
  * inside a bucket is unspecified (results are exact integer sums).
  * ------------------------------------------------------------------------- */
 size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t tile_w);
+/* The same build with a host bound nnz_cap >= nnz(C[0:n_targets]) (e.g. the
+ * raw-edge expansion count): with many mids (more than 8 * 8192) the buckets
+ * are laid out from ONE stable radix sort of (bucket, entry) pairs instead of
+ * per-entry global atomics on n_mids*T bucket counters (config4, 200 k
+ * topics); otherwise identical to dps_ct_tiles_build.  Same outputs and
+ * format; ws from dps_ct_tiles_workspace_size2. */
+size_t dps_ct_tiles_workspace_size2(int64_t n_mids, int64_t n_targets, int32_t tile_w,
+                                    int64_t nnz_cap);
+int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                        const int64_t* g, const int32_t* t_rank, int64_t n_targets, int64_t n_mids,
+                        int32_t tile_w, int64_t nnz_cap, uint32_t* tile_off, uint32_t* tile_ent,
+                        uint32_t* tile_maxc, int64_t* tile_gmin, int32_t* status_dev, void* ws,
+                        size_t ws_bytes, void* stream);
 /* Per-bucket count sums of built tiles: tile_sum[b] = sum over the bucket's
  * entries of their values (2^e of a 16-bit piece, padding codes excluded; C of
  * a 32-bit entry) = sum_{y of tile t} C[y,v] for bucket b = v*T + t, b <

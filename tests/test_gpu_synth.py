@@ -159,3 +159,47 @@ def test_bank_order_is_a_permutation(tile_w, tune):
     assert np.array_equal(a[ka], b[kb])          # same entries per bucket
     assert not np.array_equal(a, b)              # ... in a different order
     _check(eng, _oracle(t), 10)
+
+
+@pytest.mark.parametrize("tile_w", [1024, 8192, 16384, 32768])
+def test_sorted_tile_build_matches_atomic(tile_w, tune):
+    """dps_ct_tiles_build2's sorted layout (many mids: one radix sort of
+    (bucket, entry) pairs) against dps_ct_tiles_build's global-atomic counting
+    sort on the same C: identical offsets, maxima and tile minima, the same
+    multiset of entries in every bucket (order inside a bucket is free), and
+    the engine's top-k against the oracle."""
+    import torch
+    from dpathsim import _lib
+    from dpathsim.engine import build_engine
+    from dpathsim.synth import synth_dblp
+    tune(_lib.TUNE_TILE_BUILD, 2)
+    t = synth_dblp(6_000, 24_000, 20_000, seed=31).typed()
+    eng = build_engine(t, tile_w=tile_w)
+    d = eng._dev
+    NA, NV = t.n_authors, t.n_mids
+    T = (NA + tile_w - 1) // tile_w
+    off = torch.empty(NV * T + 1, dtype=torch.int32, device=eng.device)
+    mx = torch.empty_like(off)
+    gm = torch.empty(T, dtype=torch.int64, device=eng.device)
+    ent = torch.empty_like(d["tile_ent"])
+    st = torch.zeros(1, dtype=torch.int32, device=eng.device)
+    ws = torch.empty(_lib.size("dps_ct_tiles_workspace_size", NV, NA, tile_w), dtype=torch.uint8,
+                     device=eng.device)
+    _lib.call("dps_ct_tiles_build", d["c_ptr"].data_ptr(), d["c_col"].data_ptr(),
+              d["c_val"].data_ptr(), d["den"].data_ptr(), d["t_rank"].data_ptr(), NA, NV, tile_w,
+              off.data_ptr(), ent.data_ptr(), mx.data_ptr(), gm.data_ptr(), st.data_ptr(),
+              ws.data_ptr(), ws.numel(), eng.stream)
+    torch.cuda.synchronize()
+    o1 = off.cpu().numpy().astype(np.int64)
+    o2 = d["tile_off"].cpu().numpy().astype(np.int64)
+    assert np.array_equal(o1, o2)
+    assert np.array_equal(mx.cpu().numpy(), d["tile_maxc"].cpu().numpy()[: NV * T + 1])
+    assert np.array_equal(gm.cpu().numpy(), d["tile_gmin"].cpu().numpy()[:T])
+    per = 2 if tile_w <= 16384 else 1
+    n = int(o1[-1]) * per
+    view = (lambda a: a.view(np.uint16)) if per == 2 else (lambda a: a)
+    a = view(ent.cpu().numpy())[:n]
+    b = view(d["tile_ent"].cpu().numpy())[:n]
+    bucket = np.repeat(np.arange(len(o1) - 1), per * np.diff(o1))
+    assert np.array_equal(a[np.lexsort((a, bucket))], b[np.lexsort((b, bucket))])
+    _check(eng, _oracle(t), 10)
