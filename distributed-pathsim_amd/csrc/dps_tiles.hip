@@ -149,36 +149,41 @@ __global__ __launch_bounds__(kBlock) void k_round4(uint32_t* __restrict__ cnt, i
   }
 }
 
+// Padding entries i0 .. i0 + np of a bucket: C = 0 (they add nothing) and a
+// label that walks over the tile's dwords, so the hot kernel's branch-free u8
+// adds of padding do not pile onto one LDS bank.
+__device__ __forceinline__ void pad_bucket(int64_t i0, int64_t np, uint32_t lab_mask, int fmt,
+                                           uint32_t* __restrict__ ent) {
+  for (int64_t k = 0; k < np; ++k) {
+    const int64_t i = i0 + k;
+    if (fmt == kFmt32) {
+      ent[i] = (static_cast<uint32_t>(i) << 2) & lab_mask & ~3u;
+      continue;
+    }
+    // groups on one dword: {hi, lo, lo} first when the count is odd, then
+    // {hi, hi}; hi / lo = 7 / 6 (u8 counters, label % 4 == 3) or 3 / 2
+    // (4-bit counters, label % 8 == 7)
+    const bool odd = (np & 1) != 0;
+    const int64_t grp = odd ? (k < 3 ? 0 : 1 + (k - 3) / 2) : k / 2;
+    const bool u8 = fmt == kFmtU8;
+    const uint32_t hi = u8 ? 7u : 3u;
+    const uint32_t e = (odd && (k == 1 || k == 2)) ? hi - 1u : hi;
+    const uint32_t lab = u8 ? (((static_cast<uint32_t>(i0 + 2 * grp) << 2) & lab_mask & ~3u) | 3u)
+                            : (((static_cast<uint32_t>(i0 + 2 * grp) << 3) & lab_mask & ~7u) | 7u);
+    reinterpret_cast<uint16_t*>(ent)[i] = static_cast<uint16_t>((lab << ent_lsh(fmt)) | e);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_tile_pad(const int64_t* __restrict__ off, int P,
                                                      const uint32_t* __restrict__ cursor,
                                                      int64_t n, uint32_t lab_mask, int fmt,
                                                      uint32_t* __restrict__ ent) {
   // Bucket b spans off[b*P] .. off[(b+1)*P) (P parts per bucket), its first
-  // cursor[b] entries are real.  Padding entries have C = 0 (they add nothing)
-  // and a label that walks over the tile's dwords, so the hot kernel's
-  // branch-free u8 adds of padding do not pile onto one LDS bank.
+  // cursor[b] entries are real.
   for (int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; b < n;
        b += static_cast<int64_t>(gridDim.x) * kBlock) {
     const int64_t i0 = off[b * P] + cursor[b];
-    const int64_t np = off[(b + 1) * P] - i0;
-    for (int64_t k = 0; k < np; ++k) {
-      const int64_t i = i0 + k;
-      if (fmt == kFmt32) {
-        ent[i] = (static_cast<uint32_t>(i) << 2) & lab_mask & ~3u;
-        continue;
-      }
-      // groups on one dword: {hi, lo, lo} first when the count is odd, then
-      // {hi, hi}; hi / lo = 7 / 6 (u8 counters, label % 4 == 3) or 3 / 2
-      // (4-bit counters, label % 8 == 7)
-      const bool odd = (np & 1) != 0;
-      const int64_t grp = odd ? (k < 3 ? 0 : 1 + (k - 3) / 2) : k / 2;
-      const bool u8 = fmt == kFmtU8;
-      const uint32_t hi = u8 ? 7u : 3u;
-      const uint32_t e = (odd && (k == 1 || k == 2)) ? hi - 1u : hi;
-      const uint32_t lab = u8 ? (((static_cast<uint32_t>(i0 + 2 * grp) << 2) & lab_mask & ~3u) | 3u)
-                              : (((static_cast<uint32_t>(i0 + 2 * grp) << 3) & lab_mask & ~7u) | 7u);
-      reinterpret_cast<uint16_t*>(ent)[i] = static_cast<uint16_t>((lab << ent_lsh(fmt)) | e);
-    }
+    pad_bucket(i0, off[(b + 1) * P] - i0, lab_mask, fmt, ent);
   }
 }
 
@@ -873,123 +878,182 @@ __global__ __launch_bounds__(kBlock) void k_tile_sums(const uint32_t* __restrict
 // --------------------------------------------------------------------------
 // Sorted tile build (dps_ct_tiles_build2, many mids -- config4's 200k topics,
 // where the per-entry global atomics on n_mids * T bucket counters cost 5.8
-// ms): every C entry becomes a (bucket, (local label << 16) | C) pair, one
-// stable LSD radix sort orders them by bucket, and the buckets are then
-// counted, laid out and written from the sorted order -- coalesced, no
-// atomics on the 24.6 M counters.  Pairs past nnz (the capacity is a host
-// bound) carry the key nb and sort last.
+// ms).  The C entries are enumerated in target-label order (row y's entries
+// at Q[label(y)], Q the scan of the row lengths by label) as pairs
+// ((t << 32) | v, (local label << 16) | C); one stable LSD radix sort on the
+// mid bits alone then yields (v, label) order, i.e. the (v, t) buckets
+// contiguous and each bucket's entries by label.  Buckets are then counted,
+// laid out and written from the sorted order -- coalesced, no atomics on the
+// 24.6 M bucket counters.  Pairs past nnz (the capacity is a host bound)
+// carry the mid n_mids and sort last.
+__global__ __launch_bounds__(kBlock) void k_label_len(const int64_t* __restrict__ c_ptr,
+                                                      const int32_t* __restrict__ rank,
+                                                      int64_t n_rows, uint32_t* __restrict__ len) {
+  for (int64_t y = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; y < n_rows;
+       y += static_cast<int64_t>(gridDim.x) * kBlock)
+    len[label_of(rank, y)] = static_cast<uint32_t>(c_ptr[y + 1] - c_ptr[y]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_label_perm(const int32_t* __restrict__ rank,
+                                                       int64_t n_rows, int32_t* __restrict__ perm) {
+  for (int64_t y = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; y < n_rows;
+       y += static_cast<int64_t>(gridDim.x) * kBlock)
+    perm[label_of(rank, y)] = static_cast<int32_t>(y);
+}
+
+// A quarter wave (16 lanes) per target label, in label order: the rows are
+// gathered, the pairs written sequentially.
 __global__ __launch_bounds__(kBlock) void k_tile_keys(const int64_t* __restrict__ c_ptr,
                                                       const int32_t* __restrict__ c_col,
                                                       const int32_t* __restrict__ c_val,
-                                                      const int32_t* __restrict__ rank,
-                                                      const int64_t* __restrict__ g,
-                                                      int64_t n_rows, int shift, int64_t T,
+                                                      const int32_t* __restrict__ perm,
+                                                      const int64_t* __restrict__ Q,
+                                                      int64_t n_rows, int shift,
                                                       uint64_t* __restrict__ keys,
                                                       uint32_t* __restrict__ vals,
-                                                      unsigned long long* __restrict__ gmin,
                                                       int32_t* __restrict__ status) {
-  __shared__ unsigned long long gmin_s[kTileGminLds];
-  const bool lds_gmin = gmin && T <= kTileGminLds;
-  if (lds_gmin)
-    for (int64_t i = threadIdx.x; i < T; i += kBlock) gmin_s[i] = ~0ull;
-  __syncthreads();
-  const int lane = lane_id();
-  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
-  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  constexpr int kG = 16;
+  const int gl = threadIdx.x % kG;
+  const int64_t grp0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kG;
+  const int64_t ngrp = static_cast<int64_t>(gridDim.x) * (kBlock / kG);
   const uint32_t ymask = (1u << shift) - 1u;
-  for (int64_t y = wave0; y < n_rows; y += nwaves) {
-    const int64_t lab = label_of(rank, y);
-    const int64_t t = lab >> shift;
-    if (lane == 0 && gmin) {
-      if (lds_gmin) atomicMin(&gmin_s[t], static_cast<unsigned long long>(g[y]));
-      else atomicMin(&gmin[t], static_cast<unsigned long long>(g[y]));
-    }
+  for (int64_t lab = grp0; lab < n_rows; lab += ngrp) {
+    const int64_t y = perm[lab];
+    const uint64_t t = static_cast<uint64_t>(lab >> shift);
     const uint32_t l = static_cast<uint32_t>(lab) & ymask;
-    for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
+    const int64_t j0 = c_ptr[y], j1 = c_ptr[y + 1], q = Q[lab] - j0;
+    for (int64_t j = j0 + gl; j < j1; j += kG) {
       int32_t c = c_val[j];
       if (c > 0xFFFF) {
         if (status) *status = DPS_ERR_OVERFLOW;
         c = 0xFFFF;
       }
-      keys[j] = static_cast<uint64_t>(static_cast<int64_t>(c_col[j]) * T + t);
-      vals[j] = (l << 16) | static_cast<uint32_t>(c);
+      keys[q + j] = (t << 32) | static_cast<uint32_t>(c_col[j]);
+      vals[q + j] = (l << 16) | static_cast<uint32_t>(c);
     }
   }
+}
+
+// Tile t's smallest denominator term, one block per tile (no atomics).
+__global__ __launch_bounds__(kBlock) void k_tile_gmin(const int32_t* __restrict__ perm,
+                                                      const int64_t* __restrict__ g, int64_t n_rows,
+                                                      int shift, int64_t* __restrict__ gmin) {
+  __shared__ int64_t s[kBlock];
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) << shift;
+  const int64_t hi = lo + (int64_t(1) << shift) < n_rows ? lo + (int64_t(1) << shift) : n_rows;
+  int64_t m = INT64_MAX;
+  for (int64_t lab = lo + threadIdx.x; lab < hi; lab += kBlock) {
+    const int64_t v = g[perm[lab]];
+    m = v < m ? v : m;
+  }
+  s[threadIdx.x] = m;
   __syncthreads();
-  if (lds_gmin)
-    for (int64_t i = threadIdx.x; i < T; i += kBlock)
-      if (gmin_s[i] != ~0ull) atomicMin(&gmin[i], gmin_s[i]);
+  for (int o = kBlock / 2; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o && s[threadIdx.x + o] < s[threadIdx.x])
+      s[threadIdx.x] = s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) gmin[blockIdx.x] = s[0];
 }
 
 __global__ __launch_bounds__(kBlock) void k_tile_keys_pad(const int64_t* __restrict__ c_ptr,
-                                                          int64_t n_rows, int64_t cap, uint64_t nb,
+                                                          int64_t n_rows, int64_t cap, uint64_t pad,
                                                           uint64_t* __restrict__ keys,
                                                           uint32_t* __restrict__ vals) {
   const int64_t nnz = c_ptr[n_rows] - c_ptr[0];
   for (int64_t i = nnz + static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < cap;
        i += static_cast<int64_t>(gridDim.x) * kBlock) {
-    keys[i] = nb;
+    keys[i] = pad;
     vals[i] = 0;
   }
 }
 
+// Bucket of a sorted key, or -1 for padding.
+__device__ __forceinline__ int64_t key_bucket(uint64_t key, int64_t n_mids, int64_t T) {
+  const int64_t v = static_cast<int64_t>(key & 0xFFFFFFFFu);
+  return v >= n_mids ? -1 : v * T + static_cast<int64_t>(key >> 32);
+}
+
 // Per sorted pair: its pieces (0 past nnz), the first / one-past-last index of
-// its bucket's run (bstart / bend), the bucket maximum (C > 1 only: k_round4
-// style, the counts pass raises a non-empty bucket's maximum to 1).
+// its bucket's run (bstart / bend), and the bucket maximum (C > 1 only:
+// k_round4 style, the counts pass raises a non-empty bucket's maximum to 1) as
+// a segmented max over the wave's lanes -- one atomic per bucket and wave.
 __global__ __launch_bounds__(kBlock) void k_sorted_runs(const uint64_t* __restrict__ keys,
                                                         const uint32_t* __restrict__ vals,
-                                                        int64_t cap, uint64_t nb, int fmt,
-                                                        uint32_t* __restrict__ pieces,
+                                                        int64_t cap, int64_t n_mids, int64_t T,
+                                                        int fmt, uint32_t* __restrict__ pieces,
                                                         uint32_t* __restrict__ bstart,
                                                         uint32_t* __restrict__ bend,
                                                         uint32_t* __restrict__ maxc) {
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < cap;
-       i += static_cast<int64_t>(gridDim.x) * kBlock) {
-    const uint64_t b = keys[i];
-    if (b >= nb) {
+  const int lane = lane_id();
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t w0 = static_cast<int64_t>(blockIdx.x) * kBlock + (threadIdx.x & ~(kWave - 1));
+       w0 < cap; w0 += stride) {
+    const int64_t i = w0 + lane;
+    const bool valid = i < cap;
+    const uint64_t key = valid ? keys[i] : ~0ull;
+    const int64_t b = valid ? key_bucket(key, n_mids, T) : -1;
+    uint32_t m = 0;
+    if (b >= 0) {
+      const uint32_t v = vals[i];
+      const uint32_t c = v & 0xFFFFu, l = v >> 16;
+      pieces[i] = n_pieces(fmt, c, l);
+      m = c;
+      if (i == 0 || keys[i - 1] != key) bstart[b] = static_cast<uint32_t>(i);
+      if (i + 1 == cap || keys[i + 1] != key) bend[b] = static_cast<uint32_t>(i + 1);
+    } else if (valid) {
       pieces[i] = 0;
-      continue;
     }
-    const uint32_t v = vals[i];
-    const uint32_t c = v & 0xFFFFu, l = v >> 16;
-    pieces[i] = n_pieces(fmt, c, l);
-    if (i == 0 || keys[i - 1] != b) bstart[b] = static_cast<uint32_t>(i);
-    if (i + 1 == cap || keys[i + 1] != b) bend[b] = static_cast<uint32_t>(i + 1);
-    if (maxc && c > 1) atomicMax(&maxc[b], c);
+    if (!maxc) continue;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t mo = __shfl_up(m, o, kWave);
+      const uint64_t ko = __shfl_up(key, o, kWave);
+      if (lane >= o && ko == key) m = m > mo ? m : mo;
+    }
+    const uint64_t kn = __shfl_down(key, 1, kWave);
+    const bool last = lane == kWave - 1 || kn != key;
+    if (b >= 0 && last && m > 1) atomicMax(&maxc[b], m);
   }
 }
 
-// Bucket b: real pieces (kept in real[] for the padding pass) and the padded
-// count (cnt[], scanned into the layout).
+// Bucket b's padded count (cnt[], scanned into the layout).
 __global__ __launch_bounds__(kBlock) void k_sorted_counts(const uint32_t* __restrict__ bstart,
                                                           const uint32_t* __restrict__ bend,
                                                           const int64_t* __restrict__ P, int64_t nb,
                                                           uint32_t per16, uint32_t* __restrict__ cnt,
-                                                          uint32_t* __restrict__ real,
                                                           uint32_t* __restrict__ maxc) {
   for (int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; b < nb;
        b += static_cast<int64_t>(gridDim.x) * kBlock) {
     const uint32_t s0 = bstart[b], s1 = bend[b];
     const uint32_t n = s1 > s0 ? static_cast<uint32_t>(P[s1] - P[s0]) : 0u;
-    real[b] = n;
     cnt[b] = padded_count(n, per16);
     if (maxc && n > 0 && maxc[b] == 0) maxc[b] = 1;
   }
 }
 
+// Each pair's entries at its bucket's offset + the pieces before it in the
+// run; the run's last pair also writes the bucket's padding.
 __global__ __launch_bounds__(kBlock) void k_sorted_write(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals,
-                                                         int64_t cap, uint64_t nb, int fmt,
+                                                         int64_t cap, int64_t n_mids, int64_t T,
+                                                         int fmt, uint32_t lab_mask,
                                                          const int64_t* __restrict__ P,
                                                          const uint32_t* __restrict__ bstart,
                                                          const int64_t* __restrict__ off,
                                                          uint32_t* __restrict__ ent) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < cap;
        i += static_cast<int64_t>(gridDim.x) * kBlock) {
-    const uint64_t b = keys[i];
-    if (b >= nb) continue;
+    const uint64_t key = keys[i];
+    const int64_t b = key_bucket(key, n_mids, T);
+    if (b < 0) continue;
     const uint32_t v = vals[i];
-    put_entry(fmt, ent, off[b] + (P[i] - P[bstart[b]]), v & 0xFFFFu, v >> 16);
+    const int64_t p0 = P[bstart[b]];
+    put_entry(fmt, ent, off[b] + (P[i] - p0), v & 0xFFFFu, v >> 16);
+    if (i + 1 == cap || keys[i + 1] != key) {
+      const int64_t i0 = off[b] + (P[i + 1] - p0);
+      pad_bucket(i0, off[b + 1] - i0, lab_mask, fmt, ent);
+    }
   }
 }
 
@@ -1216,6 +1280,10 @@ size_t dps_ct_tiles_workspace_size2(int64_t n_mids, int64_t n_targets, int32_t t
   s += align_up(scan_workspace_size(static_cast<int64_t>(cap)));
   s += 2 * align_up((nb + 1) * sizeof(uint32_t));     // bstart, bend
   s += align_up(radix_sort_workspace_size(static_cast<int64_t>(cap)));
+  const size_t nt = static_cast<size_t>(n_targets > 0 ? n_targets : 1);
+  s += align_up((nt + 1) * sizeof(uint32_t)) + align_up((nt + 1) * sizeof(int64_t));  // len, Q
+  s += align_up(nt * sizeof(int32_t));                                                // perm
+  s += align_up(scan_workspace_size(static_cast<int64_t>(nt)));
   return base + s + 1024;
 }
 
@@ -1244,7 +1312,6 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
   const int64_t cap = nnz_cap > 0 ? nnz_cap : 1;
   Carve c(ws, ws_bytes);
   uint32_t* cnt = c.take<uint32_t>(nb + 1);
-  uint32_t* real = c.take<uint32_t>(nb + 1);
   int64_t* off64 = c.take<int64_t>(nb + 1);
   const size_t scan_b = scan_workspace_size(nb + 1);
   void* sws_b = c.take<char>(scan_b);
@@ -1260,6 +1327,12 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
   uint32_t* bend = c.take<uint32_t>(nb + 1);
   const size_t rs_bytes = radix_sort_workspace_size(cap);
   void* rws = c.take<char>(rs_bytes);
+  const int64_t nt = n_targets > 0 ? n_targets : 1;
+  uint32_t* len = c.take<uint32_t>(nt + 1);
+  int64_t* Q = c.take<int64_t>(nt + 1);
+  int32_t* perm = c.take<int32_t>(nt);
+  const size_t scan_q = scan_workspace_size(nt);
+  void* sws_q = c.take<char>(scan_q);
   DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "tiles workspace carve failed");
   const int fmt = tile_fmt(shift);
   const uint32_t per16 = fmt != kFmt32 ? 8u : 4u;
@@ -1273,24 +1346,31 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
     DPS_HIP_RET(fill_set(fs, st));
   }
   if (n_targets > 0) {
-    k_tile_keys<<<grid_for(n_targets * kWave, kBlock, 2048), kBlock, 0, st>>>(
-        c_ptr, c_col, c_val, t_rank, g, n_targets, shift, T, keys, vals,
-        reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
+    k_label_len<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(c_ptr, t_rank, n_targets, len);
     DPS_LAUNCHED();
+    k_label_perm<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(t_rank, n_targets, perm);
+    DPS_LAUNCHED();
+    DPS_HIP_RET(scan_exclusive<uint32_t>(len, Q, n_targets, sws_q, scan_q, st));
+    k_tile_keys<<<grid_for(n_targets * 16, kBlock, 8192), kBlock, 0, st>>>(
+        c_ptr, c_col, c_val, perm, Q, n_targets, shift, keys, vals, status_dev);
+    DPS_LAUNCHED();
+    if (tile_gmin) {
+      k_tile_gmin<<<static_cast<unsigned>(T), kBlock, 0, st>>>(perm, g, n_targets, shift, tile_gmin);
+      DPS_LAUNCHED();
+    }
   }
   k_tile_keys_pad<<<grid_for(cap, kBlock), kBlock, 0, st>>>(c_ptr, n_targets, cap,
-                                                           static_cast<uint64_t>(nb), keys, vals);
+                                                           static_cast<uint64_t>(n_mids), keys, vals);
   DPS_LAUNCHED();
   int key_bits = 1;
-  while ((int64_t(1) << key_bits) <= nb) ++key_bits;     // nb itself is the pad key
+  while ((int64_t(1) << key_bits) <= n_mids) ++key_bits;   // n_mids itself is the pad mid
   DPS_HIP_RET(radix_sort_pairs(keys, vals, keys_s, vals_s, cap, key_bits, rws, rs_bytes, st));
-  k_sorted_runs<<<grid_for(cap, kBlock), kBlock, 0, st>>>(keys_s, vals_s, cap,
-                                                         static_cast<uint64_t>(nb), fmt, pieces,
-                                                         bstart, bend, tile_maxc);
+  k_sorted_runs<<<grid_for(cap, kBlock), kBlock, 0, st>>>(keys_s, vals_s, cap, n_mids, T, fmt,
+                                                         pieces, bstart, bend, tile_maxc);
   DPS_LAUNCHED();
   DPS_HIP_RET(scan_exclusive<uint32_t>(pieces, P, cap, sws_e, scan_e, st));
   if (nb > 0) {
-    k_sorted_counts<<<grid_for(nb, kBlock), kBlock, 0, st>>>(bstart, bend, P, nb, per16, cnt, real,
+    k_sorted_counts<<<grid_for(nb, kBlock), kBlock, 0, st>>>(bstart, bend, P, nb, per16, cnt,
                                                             tile_maxc);
     DPS_LAUNCHED();
   }
@@ -1298,15 +1378,10 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
   k_tile_off32<<<grid_for(nb + 1, kBlock), kBlock, 0, st>>>(off64, 1, nb, fmt != kFmt32 ? 1 : 0,
                                                            tile_off);
   DPS_LAUNCHED();
-  k_sorted_write<<<grid_for(cap, kBlock), kBlock, 0, st>>>(keys_s, vals_s, cap,
-                                                          static_cast<uint64_t>(nb), fmt, P, bstart,
-                                                          off64, tile_ent);
+  k_sorted_write<<<grid_for(cap, kBlock), kBlock, 0, st>>>(keys_s, vals_s, cap, n_mids, T, fmt,
+                                                          static_cast<uint32_t>(tile_w) - 1u, P,
+                                                          bstart, off64, tile_ent);
   DPS_LAUNCHED();
-  if (nb > 0) {
-    k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(
-        off64, 1, real, nb, static_cast<uint32_t>(tile_w) - 1u, fmt, tile_ent);
-    DPS_LAUNCHED();
-  }
   return bank_order(fmt != kFmt32, nb, tile_off, tile_ent, st);
 }
 
