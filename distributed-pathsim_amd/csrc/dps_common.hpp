@@ -60,6 +60,13 @@ __device__ __forceinline__ int64_t readlane(int64_t v, int l) {
   return static_cast<int64_t>((static_cast<uint64_t>(static_cast<unsigned>(hi)) << 32) |
                               static_cast<unsigned>(lo));
 }
+// int64 of a per-lane source lane (ds_bpermute x 2; readlane needs a uniform lane)
+__device__ __forceinline__ int64_t readlane_var(int64_t v, int src) {
+  const uint64_t u = static_cast<uint64_t>(v);
+  const unsigned lo = static_cast<unsigned>(__shfl(static_cast<int>(u), src, kWave));
+  const unsigned hi = static_cast<unsigned>(__shfl(static_cast<int>(u >> 32), src, kWave));
+  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+}
 __device__ __forceinline__ double readlane(double v, int l) {
   return __longlong_as_double(readlane(static_cast<int64_t>(__double_as_longlong(v)), l));
 }
@@ -119,6 +126,38 @@ __device__ __forceinline__ int wave_owner(uint32_t excl, uint32_t i) {
     if (e <= i) j += step;
   }
   return j;
+}
+
+// Compaction of segmented-unique heads into CSR arrays, for the 64
+// consecutive segments s0 .. s0+63: their outputs are one contiguous range
+// from out_ptr[s0], walked in coalesced 64-entry strips, each lane finding its
+// segment by wave_owner (a lane per segment with a wave for long ones left a
+// serial copy loop per lane: config4 296 us).  Every lane must call it.
+__device__ __forceinline__ void compact_heads_wave(const int32_t* __restrict__ tmp,
+                                                   const int32_t* __restrict__ tmp_cnt,
+                                                   const int64_t* __restrict__ seg_ptr,
+                                                   const int64_t* __restrict__ out_ptr,
+                                                   int64_t n_seg, int32_t* __restrict__ col,
+                                                   int32_t* __restrict__ val, int64_t s0) {
+  const int lane = lane_id();
+  const int64_t sl = s0 + lane;
+  const int64_t se = sl < n_seg ? sl : n_seg;
+  const int64_t o0 = out_ptr[s0];
+  const uint32_t excl = static_cast<uint32_t>(out_ptr[se] - o0);
+  const uint32_t total =
+      static_cast<uint32_t>(out_ptr[s0 + kWave < n_seg ? s0 + kWave : n_seg] - o0);
+  const int64_t src = sl < n_seg ? seg_ptr[sl] : 0;
+  for (uint32_t e0 = 0; e0 < total; e0 += kWave) {
+    const uint32_t i = e0 + static_cast<uint32_t>(lane);
+    const int o = wave_owner(excl, i);
+    const int64_t so = readlane_var(src, o);
+    const uint32_t eo = static_cast<uint32_t>(__shfl(static_cast<int>(excl), o, kWave));
+    if (i < total) {
+      const int64_t j = so + (i - eo);
+      col[o0 + i] = tmp[j];
+      if (val) val[o0 + i] = tmp_cnt[j];
+    }
+  }
 }
 
 // Ascending bitonic sort of one int per lane across the wave.  `lane` is the
@@ -182,10 +221,20 @@ hipError_t scan_exclusive(const T* in, int64_t* out, int64_t n, void* ws, size_t
 // For every segment s: data[seg_ptr[s] .. seg_ptr[s+1]) is sorted ascending and
 // compacted in place to its distinct values (first uniq[s] slots); when
 // `counts` is non-null counts[seg_ptr[s] + i] = multiplicity of value i.
+// With a SegSrc map the input value at j is map[col[j]] (the single-mid
+// SpGEMM's paper -> mid gather, fused into the sort's loads) and data is
+// output only.
+struct SegSrc {
+  const int32_t* col = nullptr;
+  const int32_t* map = nullptr;
+};
+__device__ __forceinline__ int32_t seg_in(const int32_t* data, const SegSrc& src, int64_t j) {
+  return src.map ? src.map[src.col[j]] : data[j];
+}
 size_t seg_unique_workspace_size(int64_t n_seg);
 hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, int64_t n_seg,
                       int64_t* uniq, void* ws, size_t ws_bytes, hipStream_t stream,
-                      int key_range = 0);
+                      int key_range = 0, SegSrc src = SegSrc());
 
 // ---- stable LSD radix sort of (u64 key, u32 value) pairs (dps_sort.hip) ------
 // Sorts by the low key_bits bits of the keys; vals_in == nullptr means values

@@ -10,7 +10,11 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kSegLdsCap = 12288;  // ints staged in LDS by the long-segment path (48 KiB)
+// ints staged in LDS by the long-segment path (56 KiB of dynamic LDS; it is
+// reached through a generic pointer shared with the in-place global path, so it
+// stays below 64 KiB: a 128 KiB static array faulted there, while ds_* access to
+// 144 KiB static LDS is fine in k_col_sums_wide)
+constexpr int kSegLdsCap = 14336;
 
 __device__ __forceinline__ int64_t bound_from(const int64_t* dev, int64_t host) {
   return dev ? *dev : host;
@@ -287,75 +291,99 @@ BucketPlan bucket_plan(int64_t cap, int64_t n_rows) {
   return P;
 }
 
-// Column sums (and author-entry counts) for more mids than one LDS range: one
-// pass over the entries, each block reducing a chunk of kColChunk entries in an
-// LDS hash table (open addressing; a chunk has at most kColChunk distinct mids,
-// so the 2x-sized table never fills), then one global atomic per (block, mid)
-// -- instead of re-reading every entry once per 6144-mid range (config4: 33
-// ranges of 200k topics).
-constexpr int kColChunk = 4096;
-constexpr int kColSlots = 2 * kColChunk;
+// Column sums (and author-entry counts) for more mids than one LDS range:
+// block (x, y) reduces the mids [y*kWideMids, (y+1)*kWideMids) of entry chunk
+// x in 144 KiB of LDS (u64 sums, u32 counts; one 1024-thread block per CU),
+// then flushes one global atomic per nonzero (block, mid).  The chunks are
+// few (about two blocks per CU over all ranges), so the flush stays small;
+// every range re-reads c_col (config4: 17 ranges x 118 MB).  Replaces a
+// per-4096-entry LDS hash whose flush was one scattered global atomic per
+// entry (config4: 2.29 ms).
+constexpr int kWideBlock = 1024;
+constexpr int kWideMids = 12288;
 
-__device__ __forceinline__ uint32_t col_slot(uint32_t v) {
-  return (v * 2654435761u) >> (32 - 13);   // kColSlots = 2^13
-}
-
-__global__ __launch_bounds__(kBlock) void k_col_sums_hash(const int64_t* __restrict__ c_ptr,
-                                                          const int32_t* __restrict__ c_col,
-                                                          const int32_t* __restrict__ c_val,
-                                                          int64_t n_rows,
-                                                          unsigned long long* __restrict__ s,
-                                                          int64_t n_count_rows,
-                                                          unsigned* __restrict__ n_v) {
-  __shared__ int32_t key[kColSlots];
-  __shared__ unsigned long long sum[kColSlots];
-  __shared__ unsigned cnt[kColSlots];
+__global__ __launch_bounds__(kWideBlock) void k_col_sums_wide(const int64_t* __restrict__ c_ptr,
+                                                              const int32_t* __restrict__ c_col,
+                                                              const int32_t* __restrict__ c_val,
+                                                              int64_t n_rows, int64_t n_mids,
+                                                              unsigned long long* __restrict__ s,
+                                                              int64_t n_count_rows,
+                                                              unsigned* __restrict__ n_v) {
+  __shared__ unsigned long long h[kWideMids];
+  __shared__ unsigned hc[kWideMids];
+  const int64_t m0 = static_cast<int64_t>(blockIdx.y) * kWideMids;
+  const int m = static_cast<int>(min(static_cast<int64_t>(kWideMids), n_mids - m0));
+  for (int i = threadIdx.x; i < m; i += kWideBlock) { h[i] = 0; hc[i] = 0; }
+  __syncthreads();
   const int64_t b0 = c_ptr[0], nnz = c_ptr[n_rows] - b0;
   const int64_t ncnt = n_v ? c_ptr[n_count_rows] - b0 : 0;
-  for (int64_t j0 = static_cast<int64_t>(blockIdx.x) * kColChunk; j0 < nnz;
-       j0 += static_cast<int64_t>(gridDim.x) * kColChunk) {
-    for (int t = threadIdx.x; t < kColSlots; t += kBlock) { key[t] = -1; sum[t] = 0; cnt[t] = 0; }
-    __syncthreads();
-    const int64_t j1 = min(j0 + kColChunk, nnz);
-    for (int64_t j = j0 + threadIdx.x; j < j1; j += kBlock) {
-      const int32_t v = c_col[b0 + j];
-      uint32_t h = col_slot(static_cast<uint32_t>(v));
-      for (;;) {
-        const int32_t old = atomicCAS(&key[h], -1, v);
-        if (old == -1 || old == v) break;
-        h = (h + 1) & (kColSlots - 1);
+  // the block's entries [J0, J1) in absolute positions, read as int4 groups
+  // (groups straddling a chunk edge are read by both blocks, each taking its
+  // own entries); c_val only for the entries in range
+  const int64_t per = ((nnz + gridDim.x - 1) / gridDim.x + 3) & ~int64_t(3);
+  const int64_t J0 = b0 + min(static_cast<int64_t>(blockIdx.x) * per, nnz);
+  const int64_t J1 = b0 + min(static_cast<int64_t>(blockIdx.x + 1) * per, nnz);
+  const int64_t Jc = b0 + ncnt;
+  const int64_t Jend = b0 + nnz;
+  const bool vec = (reinterpret_cast<uintptr_t>(c_col) & 15) == 0;
+  for (int64_t q = (J0 >> 2) + threadIdx.x; (q << 2) < J1; q += kWideBlock) {
+    int32_t col4[4];
+    if (vec && (q << 2) + 4 <= Jend) {          // never past the last entry
+      const int4 cv = reinterpret_cast<const int4*>(c_col)[q];
+      col4[0] = cv.x; col4[1] = cv.y; col4[2] = cv.z; col4[3] = cv.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t j = (q << 2) + e;
+        col4[e] = (j >= J0 && j < J1) ? c_col[j] : -1;
       }
-      atomicAdd(&sum[h], static_cast<unsigned long long>(c_val[b0 + j]));
-      if (j < ncnt) atomicAdd(&cnt[h], 1u);
     }
-    __syncthreads();
-    for (int t = threadIdx.x; t < kColSlots; t += kBlock) {
-      const int32_t v = key[t];
-      if (v < 0) continue;
-      atomicAdd(&s[v], sum[t]);
-      if (n_v && cnt[t]) atomicAdd(&n_v[v], cnt[t]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t j = (q << 2) + e;
+      const uint32_t d = static_cast<uint32_t>(col4[e] - m0);
+      if (j >= J0 && j < J1 && d < static_cast<uint32_t>(m)) {
+        atomicAdd(&h[d], static_cast<unsigned long long>(c_val[j]));
+        if (j < Jc) atomicAdd(&hc[d], 1u);
+      }
     }
-    __syncthreads();
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < m; i += kWideBlock) {
+    if (h[i]) atomicAdd(&s[m0 + i], h[i]);
+    if (n_v && hc[i]) atomicAdd(&n_v[m0 + i], hc[i]);
+  }
+}
+
+__host__ __forceinline__ dim3 col_sums_wide_grid(int64_t n_mids) {
+  const unsigned ny = static_cast<unsigned>((n_mids + kWideMids - 1) / kWideMids);
+  const unsigned nx = ny >= 512 ? 1u : 512u / ny;
+  return dim3(nx, ny);
 }
 
 // ---------------------------------------------------------------------------
 // Segmented sort + unique (+ run lengths).
 // Tiny segments (2..16): one lane each, a 16-input bitonic network in registers.
 constexpr int kLaneSeg = 16;
+// medium segments (65 .. 256): one wave each, LDS bitonic.  Longer ones go to
+// the 1024-thread rank sort: a wave's bitonic over 1024 entries (55 dependent
+// LDS steps of 8 pairs per lane) took ~50 us alone and set k_seg_mid's time.
+constexpr int kMidSeg = 256;
 
+template <int N>
 __device__ __forceinline__ void lane_sort_unique(int32_t* __restrict__ data,
                                                  int32_t* __restrict__ counts, int64_t beg,
-                                                 int len, int64_t* __restrict__ uniq_out) {
-  int32_t v[kLaneSeg];
+                                                 int len, int64_t* __restrict__ uniq_out,
+                                                 const SegSrc& src) {
+  int32_t v[N];
 #pragma unroll
-  for (int i = 0; i < kLaneSeg; ++i) v[i] = i < len ? data[beg + i] : INT_MAX;
+  for (int i = 0; i < N; ++i) v[i] = i < len ? seg_in(data, src, beg + i) : INT_MAX;
 #pragma unroll
-  for (int k = 2; k <= kLaneSeg; k <<= 1) {
+  for (int k = 2; k <= N; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
 #pragma unroll
-      for (int i = 0; i < kLaneSeg; ++i) {
+      for (int i = 0; i < N; ++i) {
         const int l = i ^ j;
         if (l > i) {
           const int32_t a = v[i], b = v[l];
@@ -369,7 +397,7 @@ __device__ __forceinline__ void lane_sort_unique(int32_t* __restrict__ data,
   int u = 0;
   int run = 0;
 #pragma unroll
-  for (int i = 0; i < kLaneSeg; ++i) {
+  for (int i = 0; i < N; ++i) {
     if (i < len) {
       const bool first = i == 0 || v[i] != v[i - 1];
       if (first) {
@@ -392,10 +420,14 @@ __global__ __launch_bounds__(kBlock) void k_seg_short(int32_t* __restrict__ data
                                                       const int64_t* __restrict__ seg_ptr,
                                                       int64_t n_seg, int64_t* __restrict__ uniq,
                                                       int32_t* __restrict__ long_list,
-                                                      unsigned* __restrict__ n_long) {
+                                                      unsigned* __restrict__ n_long,
+                                                      int32_t* __restrict__ mid_list,
+                                                      unsigned* __restrict__ n_mid,
+                                                      SegSrc src) {
   // Triage 64 segments per wave, one per lane (coalesced seg_ptr reads): empty
-  // and single-element segments are finished by their lane, long ones (> 64)
-  // go to the block-level kernel, and the rest are sorted one at a time by the
+  // and single-element segments are finished by their lane, medium ones (65 ..
+  // kMidSeg, when mid_list is given) go to the wave-level kernel, long ones to
+  // the block-level kernel, and the rest are sorted one at a time by the
   // whole wave.  Most segments of the typed CSR builds are empty (non-author
   // rows) or single (one venue per paper).
   const int lane = lane_id();
@@ -410,21 +442,30 @@ __global__ __launch_bounds__(kBlock) void k_seg_short(int32_t* __restrict__ data
       ll = static_cast<int>(seg_ptr[sl + 1] - bl);
       if (ll <= 1) {
         uniq[sl] = ll;
-        if (ll == 1 && counts) counts[bl] = 1;
+        if (ll == 1) {
+          if (counts) counts[bl] = 1;
+          if (src.map) data[bl] = seg_in(data, src, bl);
+        }
       } else if (ll <= kLaneSeg) {
-        lane_sort_unique(data, counts, bl, ll, uniq + sl);
+        lane_sort_unique<kLaneSeg>(data, counts, bl, ll, uniq + sl, src);
+      } else if (ll <= 2 * kLaneSeg) {
+        // 17 .. 32 (config4's expansions: 30 on average): a 32-input network
+        // per lane -- 64 segments at once instead of one per wave
+        lane_sort_unique<2 * kLaneSeg>(data, counts, bl, ll, uniq + sl, src);
+      } else if (mid_list && ll > kWave && ll <= kMidSeg) {
+        mid_list[atomicAdd(n_mid, 1u)] = static_cast<int32_t>(sl);
       } else if (ll > kWave) {
         long_list[atomicAdd(n_long, 1u)] = static_cast<int32_t>(sl);
       }
     }
-    uint64_t todo = ballot(ll > kLaneSeg && ll <= kWave);
+    uint64_t todo = ballot(ll > 2 * kLaneSeg && ll <= kWave);
     while (todo) {
-      const int src = __ffsll(static_cast<long long>(todo)) - 1;
+      const int sl_lane = __ffsll(static_cast<long long>(todo)) - 1;
       todo &= todo - 1;
-      const int64_t s = s0 + src;
-      const int64_t beg = readlane(bl, src);
-      const int len = readlane(ll, src);
-      int v = lane < len ? data[beg + lane] : INT_MAX;
+      const int64_t s = s0 + sl_lane;
+      const int64_t beg = readlane(bl, sl_lane);
+      const int len = readlane(ll, sl_lane);
+      int v = lane < len ? seg_in(data, src, beg + lane) : INT_MAX;
       v = wave_bitonic_sort(v);
       const int prev = __shfl_up(v, 1, kWave);
       const bool first = lane < len && (lane == 0 || v != prev);
@@ -440,6 +481,94 @@ __global__ __launch_bounds__(kBlock) void k_seg_short(int32_t* __restrict__ data
       }
       if (lane == 0) uniq[s] = __popcll(mask);
     }
+  }
+}
+
+// Medium segments (65 .. kMidSeg): one wave each, staged in 1 KiB of LDS,
+// bitonic network with virtual +inf padding (as block_bitonic_sort, at wave
+// scope), then unique (+ run lengths) in 64-entry strips.  A 1024-thread
+// block per segment (k_seg_long) left 90 % of its threads idle on config4's
+// 54 k segments of about 114 entries.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(kBlock) void k_seg_mid(int32_t* __restrict__ data,
+                                                    int32_t* __restrict__ counts,
+                                                    const int64_t* __restrict__ seg_ptr,
+                                                    int64_t* __restrict__ uniq,
+                                                    const int32_t* __restrict__ mid_list,
+                                                    const unsigned* __restrict__ n_mid,
+                                                    SegSrc src) {
+  __shared__ int32_t buf[kWavesPerBlock][kMidSeg];
+  const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
+  int32_t* a = buf[wave];
+  const unsigned nm = *n_mid;
+  const unsigned nwaves = gridDim.x * kWavesPerBlock;
+  for (unsigned li = blockIdx.x * kWavesPerBlock + wave; li < nm; li += nwaves) {
+    const int64_t sg = mid_list[li];
+    const int64_t beg = seg_ptr[sg];
+    const int len = static_cast<int>(seg_ptr[sg + 1] - beg);
+    for (int i = lane; i < len; i += kWave) a[i] = seg_in(data, src, beg + i);
+    wave_lds_sync();
+    int n2 = kWave;
+    while (n2 < len) n2 <<= 1;
+    const int half_n = n2 >> 1;
+    for (int k = 2; k <= n2; k <<= 1) {
+      const int half = k >> 1;
+      for (int p = lane; p < half_n; p += kWave) {
+        const int blk = p / half, off = p - blk * half;
+        const int i = blk * k + off, j = blk * k + k - 1 - off;
+        if (j < len) {
+          const int32_t ai = a[i], aj = a[j];
+          if (aj < ai) { a[i] = aj; a[j] = ai; }
+        }
+      }
+      wave_lds_sync();
+      for (int jd = half >> 1; jd > 0; jd >>= 1) {
+        for (int p = lane; p < half_n; p += kWave) {
+          const int blk = p / jd, off = p - blk * jd;
+          const int i = blk * 2 * jd + off, j = i + jd;
+          if (j < len) {
+            const int32_t ai = a[i], aj = a[j];
+            if (aj < ai) { a[i] = aj; a[j] = ai; }
+          }
+        }
+        wave_lds_sync();
+      }
+    }
+    int carry = 0;
+    for (int c0 = 0; c0 < len; c0 += kWave) {
+      const int i = c0 + lane;
+      const bool valid = i < len;
+      const int32_t v = valid ? a[i] : 0;
+      const bool first = valid && (i == 0 || v != a[i - 1]);
+      const uint64_t mask = ballot(first);
+      if (first) {
+        const int r = carry + mbcnt(mask);
+        data[beg + r] = v;
+        if (counts) {
+          // run length: next head in this strip, else the strip's first head
+          // of the next one is found below through the position array
+          const uint64_t above = mask & ~((2ull << lane) - 1ull);
+          int next;
+          if (above) {
+            next = c0 + __ffsll(static_cast<long long>(above)) - 1;
+          } else {
+            next = len;
+            for (int q = c0 + kWave; q < len; ++q)
+              if (a[q] != a[q - 1]) { next = q; break; }
+          }
+          counts[beg + r] = next - i;
+        }
+      }
+      carry += __popcll(mask);
+    }
+    if (lane == 0) uniq[sg] = carry;
+    wave_lds_sync();
   }
 }
 
@@ -507,7 +636,8 @@ __global__ __launch_bounds__(kLongBlock) void k_seg_long(int32_t* __restrict__ d
                                                          int64_t* __restrict__ uniq,
                                                          const int32_t* __restrict__ long_list,
                                                          const unsigned* __restrict__ n_long,
-                                                         unsigned* __restrict__ next) {
+                                                         unsigned* __restrict__ next,
+                                                         SegSrc src) {
   extern __shared__ __attribute__((aligned(16))) int32_t lds_seg[];
   constexpr int kNW = kLongBlock / kWave;
   __shared__ int64_t lds_w[kNW];
@@ -530,7 +660,7 @@ __global__ __launch_bounds__(kLongBlock) void k_seg_long(int32_t* __restrict__ d
       // rank sort (no barrier per phase): element i goes to the number of
       // elements before it in (value, index) order; 4 values per LDS read
       const int i = threadIdx.x;
-      const int32_t x = i < len ? data[beg + i] : INT_MAX;
+      const int32_t x = i < len ? seg_in(data, src, beg + i) : INT_MAX;
       const int len4 = (len + 3) & ~3;
       lds_seg[i] = x;                              // padding: INT_MAX at index >= len
       __syncthreads();
@@ -546,12 +676,16 @@ __global__ __launch_bounds__(kLongBlock) void k_seg_long(int32_t* __restrict__ d
       __syncthreads();
       a = lds_seg + kRankSortMax;
     } else if (len <= kSegLdsCap) {
-      for (int i = threadIdx.x; i < len; i += kLongBlock) lds_seg[i] = data[beg + i];
+      for (int i = threadIdx.x; i < len; i += kLongBlock) lds_seg[i] = seg_in(data, src, beg + i);
       __syncthreads();
       a = lds_seg;
       block_bitonic_sort(a, len);
     } else {
       a = data + beg;
+      if (src.map) {                      // gather the segment into place first
+        for (int i = threadIdx.x; i < len; i += kLongBlock) a[i] = seg_in(data, src, beg + i);
+        __syncthreads();
+      }
       block_bitonic_sort(a, len);
     }
     int64_t carry = 0;
@@ -603,7 +737,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_long_hist(int32_t* __restrict__ 
                                                           int64_t* __restrict__ uniq,
                                                           const int32_t* __restrict__ long_list,
                                                           const unsigned* __restrict__ n_long,
-                                                          int key_range) {
+                                                          int key_range, SegSrc src) {
   __shared__ uint32_t hist[kHistKeys + 1];
   __shared__ int64_t lds_w[kWavesPerBlock];
   const int nb = key_range + 1;                      // bin key_range: INT_MAX
@@ -618,7 +752,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_long_hist(int32_t* __restrict__ 
     for (int b = threadIdx.x; b < nb; b += kBlock) hist[b] = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < len; i += kBlock) {
-      const int32_t v = data[beg + i];
+      const int32_t v = seg_in(data, src, beg + i);
       atomicAdd(&hist[v < key_range ? v : key_range], 1u);
     }
     __syncthreads();
@@ -648,35 +782,10 @@ __global__ __launch_bounds__(kBlock) void k_compact(const int32_t* __restrict__ 
                                                     const int64_t* __restrict__ out_ptr,
                                                     int64_t n_seg, int32_t* __restrict__ col,
                                                     int32_t* __restrict__ val) {
-  // lane per segment for short ones (<= 8 heads), whole wave for the rest
-  const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
-  for (int64_t s0 = wave0 * kWave; s0 < n_seg; s0 += nwaves * kWave) {
-    const int64_t sl = s0 + lane;
-    int64_t src = 0, dst = 0, len = 0;
-    if (sl < n_seg) {
-      src = seg_ptr[sl];
-      dst = out_ptr[sl];
-      len = out_ptr[sl + 1] - dst;
-      if (len <= 8) {
-        for (int64_t i = 0; i < len; ++i) {
-          col[dst + i] = tmp[src + i];
-          if (val) val[dst + i] = tmp_cnt[src + i];
-        }
-      }
-    }
-    uint64_t todo = ballot(len > 8);
-    while (todo) {
-      const int l = __ffsll(static_cast<long long>(todo)) - 1;
-      todo &= todo - 1;
-      const int64_t so = readlane(src, l), d0 = readlane(dst, l), n = readlane(len, l);
-      for (int64_t i = lane; i < n; i += kWave) {
-        col[d0 + i] = tmp[so + i];
-        if (val) val[d0 + i] = tmp_cnt[so + i];
-      }
-    }
-  }
+  for (int64_t s0 = wave0 * kWave; s0 < n_seg; s0 += nwaves * kWave)
+    compact_heads_wave(tmp, tmp_cnt, seg_ptr, out_ptr, n_seg, col, val, s0);
 }
 
 __global__ void k_copy_scalar(const int64_t* src, int64_t* dst) { *dst = *src; }
@@ -687,6 +796,33 @@ __device__ __forceinline__ int64_t out_row_src(const int32_t* rows, int64_t i) {
   return rows ? static_cast<int64_t>(rows[i]) : i;
 }
 
+// Both expansion kernels: a wave owns 64 consecutive output rows and walks
+// the concatenation of their AP segments in 64-entry strips (a lane finds its
+// row by a binary search over the segment offsets, wave_owner), one paper per
+// lane.  A lane per row with the wave taking rows of more than 32 papers left
+// each lane a serial chain of dependent loads per paper (config4: 582 us for
+// the expansion, 160 us for its lengths).
+struct ApStrips {
+  int64_t b;        // this lane's row: first AP entry, ...
+  uint32_t excl;    // ... its offset in the wave's concatenation
+  uint32_t total;   // the wave's AP entries
+};
+__device__ __forceinline__ ApStrips ap_strips(const int64_t* __restrict__ ap_ptr,
+                                              const int32_t* __restrict__ rows, int64_t x,
+                                              int64_t n_out) {
+  ApStrips a{0, 0, 0};
+  uint32_t len = 0;
+  if (x < n_out) {
+    const int64_t r = out_row_src(rows, x);
+    a.b = ap_ptr[r];
+    len = static_cast<uint32_t>(ap_ptr[r + 1] - a.b);
+  }
+  const uint32_t incl = wave_inclusive_sum(len);
+  a.excl = incl - len;
+  a.total = readlane(incl, kWave - 1);
+  return a;
+}
+
 __global__ __launch_bounds__(kBlock) void k_expand_len(const int64_t* __restrict__ ap_ptr,
                                                        const int32_t* __restrict__ ap_col,
                                                        const int32_t* __restrict__ rows,
@@ -694,50 +830,39 @@ __global__ __launch_bounds__(kBlock) void k_expand_len(const int64_t* __restrict
                                                        const int64_t* __restrict__ px_ptr,
                                                        int64_t* __restrict__ e_len,
                                                        unsigned long long* e_total) {
-  // lane per output row for rows of <= 32 papers, whole wave for longer rows;
-  // one atomic per wave for the total
+  // per-row sums in LDS by owner lane; one atomic per block for the total
+  __shared__ unsigned long long acc[kWavesPerBlock][kWave];
   const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
   int64_t lane_total = 0;
   for (int64_t i0 = wave0 * kWave; i0 < n_out; i0 += nwaves * kWave) {
-    const int64_t i = i0 + lane;
-    int64_t b = 0, e = 0;
-    if (i < n_out) {
-      const int64_t r = out_row_src(rows, i);
-      b = ap_ptr[r];
-      e = ap_ptr[r + 1];
-      if (e - b <= 32) {
-        int64_t sum = 0;
-        for (int64_t j = b; j < e; ++j) {
-          const int32_t p = ap_col[j];
-          sum += px_ptr[p + 1] - px_ptr[p];
-        }
-        lane_total += sum;
-        if (e_len) e_len[i] = sum;
+    const int64_t x = i0 + lane;
+    const ApStrips a = ap_strips(ap_ptr, rows, x, n_out);
+    acc[wave][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t e0 = 0; e0 < a.total; e0 += kWave) {
+      const uint32_t i = e0 + static_cast<uint32_t>(lane);
+      const int o = wave_owner(a.excl, i);   // every lane takes part in the shuffles
+      const int64_t bo = readlane_var(a.b, o);
+      const uint32_t eo = static_cast<uint32_t>(__shfl(static_cast<int>(a.excl), o, kWave));
+      if (i < a.total) {
+        const int32_t p = ap_col[bo + (i - eo)];
+        const int64_t c = px_ptr[p + 1] - px_ptr[p];
+        if (c) atomicAdd(&acc[wave][o], static_cast<unsigned long long>(c));
+        lane_total += c;
       }
     }
-    uint64_t todo = ballot(e - b > 32);
-    while (todo) {
-      const int l = __ffsll(static_cast<long long>(todo)) - 1;
-      todo &= todo - 1;
-      const int64_t bb = readlane(b, l), ee = readlane(e, l);
-      int64_t sum = 0;
-      for (int64_t j = bb + lane; j < ee; j += kWave) {
-        const int32_t p = ap_col[j];
-        sum += px_ptr[p + 1] - px_ptr[p];
-      }
-      sum = wave_sum(sum);
-      if (lane == 0) {
-        lane_total += sum;
-        if (e_len) e_len[i0 + l] = sum;
-      }
-    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (x < n_out && e_len) e_len[x] = static_cast<int64_t>(acc[wave][lane]);
+    __builtin_amdgcn_wave_barrier();
   }
-  // one atomic per block on the (hot) total
   __shared__ int64_t part[kWavesPerBlock];
   const int64_t wave_total = wave_sum(lane_total);
-  if (lane == 0) part[threadIdx.x / kWave] = wave_total;
+  if (lane == 0) part[wave] = wave_total;
   __syncthreads();
   if (threadIdx.x == 0 && e_total) {
     int64_t t = 0;
@@ -754,45 +879,30 @@ __global__ __launch_bounds__(kBlock) void k_expand(const int64_t* __restrict__ a
                                                    const int32_t* __restrict__ px_col,
                                                    const int64_t* __restrict__ exp_ptr,
                                                    int32_t* __restrict__ tmp) {
-  // 64 output rows per wave: a lane expands its own row when the row has at
-  // most 32 papers (the common case), the whole wave expands longer rows
+  // the expansion of rows i0 .. i0+63 is contiguous from exp_ptr[i0], in the
+  // order of the concatenated AP entries: a running carry + a wave scan of the
+  // papers' mid counts place each paper's mids
   const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
   for (int64_t i0 = wave0 * kWave; i0 < n_out; i0 += nwaves * kWave) {
-    const int64_t i = i0 + lane;
-    int64_t b = 0, e = 0, out = 0;
-    if (i < n_out) {
-      const int64_t r = out_row_src(rows, i);
-      b = ap_ptr[r];
-      e = ap_ptr[r + 1];
-      out = exp_ptr[i];
-      if (e - b <= 32) {
-        for (int64_t j = b; j < e; ++j) {
-          const int32_t p = ap_col[j];
-          for (int64_t t = px_ptr[p]; t < px_ptr[p + 1]; ++t) tmp[out++] = px_col[t];
-        }
+    const ApStrips a = ap_strips(ap_ptr, rows, i0 + lane, n_out);
+    int64_t carry = exp_ptr[i0];
+    for (uint32_t e0 = 0; e0 < a.total; e0 += kWave) {
+      const uint32_t i = e0 + static_cast<uint32_t>(lane);
+      const int o = wave_owner(a.excl, i);
+      const int64_t bo = readlane_var(a.b, o);
+      const uint32_t eo = static_cast<uint32_t>(__shfl(static_cast<int>(a.excl), o, kWave));
+      int64_t pb = 0, pl = 0;
+      if (i < a.total) {
+        const int32_t p = ap_col[bo + (i - eo)];
+        pb = px_ptr[p];
+        pl = px_ptr[p + 1] - pb;
       }
-    }
-    uint64_t todo = ballot(e - b > 32);
-    while (todo) {
-      const int l = __ffsll(static_cast<long long>(todo)) - 1;
-      todo &= todo - 1;
-      const int64_t bb = readlane(b, l), ee = readlane(e, l);
-      int64_t o = readlane(out, l);
-      for (int64_t c0 = bb; c0 < ee; c0 += kWave) {
-        const int64_t j = c0 + lane;
-        int64_t pb = 0, pl = 0;
-        if (j < ee) {
-          const int32_t p = ap_col[j];
-          pb = px_ptr[p];
-          pl = px_ptr[p + 1] - pb;
-        }
-        const int64_t inc = wave_inclusive_sum(pl);
-        int64_t w = o + inc - pl;
-        for (int64_t t = 0; t < pl; ++t) tmp[w + t] = px_col[pb + t];
-        o += readlane(inc, kWave - 1);
-      }
+      const int64_t inc = wave_inclusive_sum(pl);
+      const int64_t w = carry + inc - pl;
+      for (int64_t t = 0; t < pl; ++t) tmp[w + t] = px_col[pb + t];
+      carry += readlane(inc, kWave - 1);
     }
   }
 }
@@ -1016,30 +1126,38 @@ __global__ __launch_bounds__(kBlock) void k_col_sums(const int64_t* __restrict__
 
 // ---------------------------------------------------------------------------
 size_t seg_unique_workspace_size(int64_t n_seg) {
-  return align_up(static_cast<size_t>(n_seg > 0 ? n_seg : 1) * sizeof(int32_t)) + 256;
+  return 2 * align_up(static_cast<size_t>(n_seg > 0 ? n_seg : 1) * sizeof(int32_t)) + 512;
 }
 
 hipError_t seg_unique(int32_t* data, int32_t* counts, const int64_t* seg_ptr, int64_t n_seg,
                       int64_t* uniq, void* ws, size_t ws_bytes, hipStream_t stream,
-                      int key_range) {
+                      int key_range, SegSrc src) {
   Carve c(ws, ws_bytes);
   int32_t* long_list = c.take<int32_t>(n_seg > 0 ? n_seg : 1);
-  unsigned* n_long = c.take<unsigned>(2);   // [0] list length, [1] queue head
+  int32_t* mid_list = c.take<int32_t>(n_seg > 0 ? n_seg : 1);
+  unsigned* n_long = c.take<unsigned>(4);   // [0] long list length, [1] queue head, [2] medium
   if (!c.ok) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(n_long, 0, 2 * sizeof(unsigned), stream);
+  hipError_t e = hipMemsetAsync(n_long, 0, 4 * sizeof(unsigned), stream);
   if (e != hipSuccess) return e;
   if (n_seg <= 0) return hipSuccess;
-  k_seg_short<<<grid_for(n_seg, kBlock), kBlock, 0, stream>>>(data, counts, seg_ptr,
-                                                                      n_seg, uniq, long_list,
-                                                                      n_long);
+  // small key range: every segment over 64 goes to the LDS-histogram kernel
+  const bool hist = key_range > 0 && key_range <= kHistKeys;
+  k_seg_short<<<grid_for(n_seg, kBlock), kBlock, 0, stream>>>(
+      data, counts, seg_ptr, n_seg, uniq, long_list, n_long, hist ? nullptr : mid_list, n_long + 2,
+      src);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (key_range > 0 && key_range <= kHistKeys) {
+  if (!hist) {
+    k_seg_mid<<<2048, kBlock, 0, stream>>>(data, counts, seg_ptr, uniq, mid_list, n_long + 2,
+                                           src);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (hist) {
     k_seg_long_hist<<<1024, kBlock, 0, stream>>>(data, counts, seg_ptr, uniq, long_list, n_long,
-                                                 key_range);
+                                                 key_range, src);
     return hipGetLastError();
   }
   k_seg_long<<<512, kLongBlock, kSegLdsCap * sizeof(int32_t), stream>>>(
-      data, counts, seg_ptr, uniq, long_list, n_long, n_long + 1);
+      data, counts, seg_ptr, uniq, long_list, n_long, n_long + 1, src);
   return hipGetLastError();
 }
 
@@ -1305,9 +1423,9 @@ int dps_walks_fused(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c
   }
   if (n_mids > 0) {
     if (n_rows > 0 && n_mids > kSumLds) {
-      k_col_sums_hash<<<1024, kBlock, 0, st>>>(c_ptr, c_col, c_val, n_rows,
-                                               reinterpret_cast<unsigned long long*>(s),
-                                               n_authors, n_v);
+      k_col_sums_wide<<<col_sums_wide_grid(n_mids), kWideBlock, 0, st>>>(
+          c_ptr, c_col, c_val, n_rows, n_mids, reinterpret_cast<unsigned long long*>(s), n_authors,
+          n_v);
       DPS_LAUNCHED();
     } else if (n_rows > 0) {
       k_col_sums<<<512, kBlock, 0, st>>>(c_ptr, c_col, c_val, n_rows, n_mids,
@@ -1332,8 +1450,8 @@ int dps_col_sums(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_va
   DPS_HIP_RET(hipMemsetAsync(s, 0, n_mids * sizeof(int64_t), st));
   if (n_rows == 0) return DPS_OK;
   if (n_mids > kSumLds) {
-    k_col_sums_hash<<<1024, kBlock, 0, st>>>(c_ptr, c_col, c_val, n_rows,
-                                             reinterpret_cast<unsigned long long*>(s), 0, nullptr);
+    k_col_sums_wide<<<col_sums_wide_grid(n_mids), kWideBlock, 0, st>>>(
+        c_ptr, c_col, c_val, n_rows, n_mids, reinterpret_cast<unsigned long long*>(s), 0, nullptr);
   } else {
     k_col_sums<<<512, kBlock, 0, st>>>(c_ptr, c_col, c_val, n_rows, n_mids,
                                        reinterpret_cast<unsigned long long*>(s), 0, nullptr);

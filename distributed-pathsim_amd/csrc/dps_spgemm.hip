@@ -439,12 +439,12 @@ __global__ void k_total(const int64_t* c_ptr, int64_t n, int64_t* nnz) { *nnz = 
 
 // ---- single-mid path: every paper has at most one mid ----------------------
 // The expansion of row a is then exactly its AP segment with every paper
-// replaced by its mid (or by INT_MAX when it has none), so it is built with
-// one coalesced gather per AP entry; a segmented sort + unique over the AP
-// segments (seg_unique) gives the distinct mids and their counts.
+// replaced by its mid (or by INT_MAX when it has none): a segmented sort +
+// unique over the AP segments (seg_unique) whose loads gather vp[ap_col[j]]
+// gives the distinct mids and their counts.
 // mid of every paper (INT_MAX: none), coalesced over the PX rows, so the
-// per-entry gather below is one random 4-byte read instead of three dependent
-// ones
+// per-entry gather in the segmented sort's loads is one random 4-byte read
+// instead of three dependent ones
 __global__ __launch_bounds__(kBlock) void k_paper_mid(const int64_t* __restrict__ px_ptr,
                                                       const int32_t* __restrict__ px_col,
                                                       int64_t n_papers, int32_t* __restrict__ vp) {
@@ -453,17 +453,6 @@ __global__ __launch_bounds__(kBlock) void k_paper_mid(const int64_t* __restrict_
     const int64_t q = px_ptr[p];
     vp[p] = px_ptr[p + 1] > q ? px_col[q] : INT_MAX;
   }
-}
-
-__global__ __launch_bounds__(kBlock) void k_mid_of_entry(const int64_t* __restrict__ ap_ptr,
-                                                         const int32_t* __restrict__ ap_col,
-                                                         int64_t n_rows,
-                                                         const int32_t* __restrict__ vp,
-                                                         int32_t* __restrict__ mids) {
-  const int64_t j0 = ap_ptr[0], nnz_ap = ap_ptr[n_rows];   // the capacity past it is unset
-  for (int64_t j = j0 + static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; j < nnz_ap;
-       j += static_cast<int64_t>(gridDim.x) * kBlock)
-    mids[j] = vp[ap_col[j]];
 }
 
 // Paper -> mid map straight from the typed PX pairs (no PX CSR): with at most
@@ -504,27 +493,10 @@ __global__ __launch_bounds__(kBlock) void k_compact_mids(const int32_t* __restri
                                                          const int64_t* __restrict__ c_ptr,
                                                          int64_t n_seg, int32_t* __restrict__ col,
                                                          int32_t* __restrict__ val) {
-  const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
-  for (int64_t s0 = wave0 * kWave; s0 < n_seg; s0 += nwaves * kWave) {
-    const int64_t sl = s0 + lane;
-    int64_t src = 0, dst = 0, len = 0;
-    if (sl < n_seg) {
-      src = seg_ptr[sl];
-      dst = c_ptr[sl];
-      len = c_ptr[sl + 1] - dst;
-      if (len <= 8)
-        for (int64_t i = 0; i < len; ++i) { col[dst + i] = mids[src + i]; val[dst + i] = cnt[src + i]; }
-    }
-    uint64_t todo = ballot(len > 8);
-    while (todo) {
-      const int l = __ffsll(static_cast<long long>(todo)) - 1;
-      todo &= todo - 1;
-      const int64_t so = readlane(src, l), d0 = readlane(dst, l), n = readlane(len, l);
-      for (int64_t i = lane; i < n; i += kWave) { col[d0 + i] = mids[so + i]; val[d0 + i] = cnt[so + i]; }
-    }
-  }
+  for (int64_t s0 = wave0 * kWave; s0 < n_seg; s0 += nwaves * kWave)
+    compact_heads_wave(mids, cnt, seg_ptr, c_ptr, n_seg, col, val, s0);
 }
 
 }  // namespace
@@ -617,11 +589,13 @@ int dps_spgemm_single_map(const int64_t* ap_ptr, const int32_t* ap_col, int64_t 
         k_paper_mid<<<grid_for(n_papers, kBlock), kBlock, 0, st>>>(px_ptr, px_col, n_papers, vp);
         DPS_LAUNCHED();
       }
-      k_mid_of_entry<<<grid_for(nnz_ap_cap, kBlock), kBlock, 0, st>>>(ap_ptr, ap_col, n_out_rows,
-                                                                     vp, mids);
-      DPS_LAUNCHED();
+      // the paper -> mid gather happens in the segmented sort's loads
+      // (SegSrc): mids is written only with each row's distinct mids
+      SegSrc src;
+      src.col = ap_col;
+      src.map = vp;
       DPS_HIP_RET(seg_unique(mids, cnt, ap_ptr, n_out_rows, uniq, gws, seg_ws, st,
-                             n_mids < INT32_MAX ? static_cast<int>(n_mids) : 0));
+                             n_mids < INT32_MAX ? static_cast<int>(n_mids) : 0, src));
       k_drop_none<<<grid_for(n_out_rows, kBlock), kBlock, 0, st>>>(mids, ap_ptr, n_out_rows, uniq);
       DPS_LAUNCHED();
     }

@@ -878,7 +878,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_sums(const uint32_t* __restrict
 // --------------------------------------------------------------------------
 // Sorted tile build (dps_ct_tiles_build2, many mids -- config4's 200k topics,
 // where the per-entry global atomics on n_mids * T bucket counters cost 5.8
-// ms).  The C entries are enumerated in target-label order (row y's entries
+// ms).  The C entries are laid out in target-label order (row y's entries
 // at Q[label(y)], Q the scan of the row lengths by label) as pairs
 // ((t << 32) | v, (local label << 16) | C); one stable LSD radix sort on the
 // mid bits alone then yields (v, label) order, i.e. the (v, t) buckets
@@ -901,35 +901,60 @@ __global__ __launch_bounds__(kBlock) void k_label_perm(const int32_t* __restrict
     perm[label_of(rank, y)] = static_cast<int32_t>(y);
 }
 
-// A quarter wave (16 lanes) per target label, in label order: the rows are
-// gathered, the pairs written sequentially.
+// A wave per 64 consecutive rows y, load-balanced over their entries (one
+// contiguous range of C, read in coalesced 64-entry strips; a lane finds its
+// row by a binary search over the lanes' row offsets, ds_bpermute), each entry
+// written to its label's run: Q[label(y)] + its offset in the row.  Measured
+// on config4 (29.4 M entries): 291 us, against 392 us for a wave per label in
+// label order (gathered rows, sequential writes), 650 us for a quarter wave
+// per label and 1.8-2.6 ms for the load-balanced walk in label order.
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int src) {
+  return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src << 2, static_cast<int>(v)));
+}
+
 __global__ __launch_bounds__(kBlock) void k_tile_keys(const int64_t* __restrict__ c_ptr,
                                                       const int32_t* __restrict__ c_col,
                                                       const int32_t* __restrict__ c_val,
-                                                      const int32_t* __restrict__ perm,
+                                                      const int32_t* __restrict__ rank,
                                                       const int64_t* __restrict__ Q,
                                                       int64_t n_rows, int shift,
                                                       uint64_t* __restrict__ keys,
                                                       uint32_t* __restrict__ vals,
                                                       int32_t* __restrict__ status) {
-  constexpr int kG = 16;
-  const int gl = threadIdx.x % kG;
-  const int64_t grp0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kG;
-  const int64_t ngrp = static_cast<int64_t>(gridDim.x) * (kBlock / kG);
+  const int lane = lane_id();
+  const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * (kBlock / kWave);
   const uint32_t ymask = (1u << shift) - 1u;
-  for (int64_t lab = grp0; lab < n_rows; lab += ngrp) {
-    const int64_t y = perm[lab];
-    const uint64_t t = static_cast<uint64_t>(lab >> shift);
-    const uint32_t l = static_cast<uint32_t>(lab) & ymask;
-    const int64_t j0 = c_ptr[y], j1 = c_ptr[y + 1], q = Q[lab] - j0;
-    for (int64_t j = j0 + gl; j < j1; j += kG) {
-      int32_t c = c_val[j];
-      if (c > 0xFFFF) {
-        if (status) *status = DPS_ERR_OVERFLOW;
-        c = 0xFFFF;
+  for (int64_t r0 = wave0 * kWave; r0 < n_rows; r0 += nwaves * kWave) {
+    const int64_t x = r0 + lane;
+    const int64_t base = c_ptr[r0];
+    const int64_t xe = x < n_rows ? x : n_rows;
+    const uint32_t excl = static_cast<uint32_t>(c_ptr[xe] - base);
+    const uint32_t total =
+        static_cast<uint32_t>(c_ptr[r0 + kWave < n_rows ? r0 + kWave : n_rows] - base);
+    const uint32_t labx = x < n_rows ? static_cast<uint32_t>(label_of(rank, x)) : 0u;
+    // destination of strip entry i of row x: Q[label] + (i - excl), kept mod 2^32
+    // (the capacity is below 2^32) relative to the strip
+    const uint32_t qrel = static_cast<uint32_t>((x < n_rows ? Q[labx] : 0) - excl);
+    for (uint32_t e0 = 0; e0 < total; e0 += kWave) {   // wave-uniform: every lane permutes
+      const uint32_t i = e0 + static_cast<uint32_t>(lane);
+      int k = 0;
+#pragma unroll
+      for (int step = kWave / 2; step > 0; step >>= 1)
+        if (lane_u32(excl, k + step) <= i) k += step;
+      const uint32_t lb = lane_u32(labx, k), qk = lane_u32(qrel, k);
+      if (i < total) {
+        const int64_t j = base + i;
+        uint32_t c = static_cast<uint32_t>(c_val[j]);
+        const uint32_t v = static_cast<uint32_t>(c_col[j]);
+        if (c > 0xFFFFu) {
+          if (status) *status = DPS_ERR_OVERFLOW;
+          c = 0xFFFFu;
+        }
+        const int64_t d = static_cast<int64_t>(qk + i);
+        keys[d] = (static_cast<uint64_t>(lb >> shift) << 32) | v;
+        vals[d] = ((lb & ymask) << 16) | c;
       }
-      keys[q + j] = (t << 32) | static_cast<uint32_t>(c_col[j]);
-      vals[q + j] = (l << 16) | static_cast<uint32_t>(c);
     }
   }
 }
@@ -1351,8 +1376,8 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
     k_label_perm<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(t_rank, n_targets, perm);
     DPS_LAUNCHED();
     DPS_HIP_RET(scan_exclusive<uint32_t>(len, Q, n_targets, sws_q, scan_q, st));
-    k_tile_keys<<<grid_for(n_targets * 16, kBlock, 8192), kBlock, 0, st>>>(
-        c_ptr, c_col, c_val, perm, Q, n_targets, shift, keys, vals, status_dev);
+    k_tile_keys<<<grid_for((n_targets + kWave - 1) / kWave * kWave, kBlock, 4096), kBlock, 0, st>>>(
+        c_ptr, c_col, c_val, t_rank, Q, n_targets, shift, keys, vals, status_dev);
     DPS_LAUNCHED();
     if (tile_gmin) {
       k_tile_gmin<<<static_cast<unsigned>(T), kBlock, 0, st>>>(perm, g, n_targets, shift, tile_gmin);

@@ -6,13 +6,16 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_fused_walks_match_separate_entry_points():
+@pytest.mark.parametrize("n_mids", [500, 20_000, 40_000])
+def test_fused_walks_match_separate_entry_points(n_mids):
+    """500 mids: the LDS column sums of one range; 20k / 40k: the range-blocked
+    wide kernel (mids over several 12288-mid LDS ranges, the last one partial)."""
     import torch
     import pathsim_oracle as po
     from dpathsim import _lib
     from dpathsim.engine import build_engine
     from dpathsim.synth import synth_dblp
-    t = synth_dblp(20_000, 60_000, 500, seed=13).typed()
+    t = synth_dblp(20_000, 60_000, n_mids, seed=13).typed()
     eng = build_engine(t)
     co = po.COracle.from_typed(t)
     cp, cc, cv, s_o, g_o = co.export()
@@ -29,7 +32,7 @@ def test_fused_walks_match_separate_entry_points():
     _lib.call("dps_row_work", d["c_ptr"].data_ptr(), d["c_col"].data_ptr(), na, nv,
               ncol.data_ptr(), terms.data_ptr(), st)
     assert torch.equal(s, d["s"][:nv])
-    assert torch.equal(terms, d["row_terms"][:na])
+    assert torch.equal(terms, d["row_terms"][:na])   # the fused pass's n_v (author entries per mid)
     # row work = sum over the row's venues of the author entries per venue
     n_v = np.bincount(cc[: cp[na]], minlength=nv)
     expect = np.add.reduceat(n_v[cc[: cp[na]]], cp[:na]) * (np.diff(cp[: na + 1]) > 0)
