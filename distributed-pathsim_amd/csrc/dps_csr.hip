@@ -136,6 +136,13 @@ __global__ __launch_bounds__(kBlock) void k_scatter_rows(
 constexpr int kL1Chunk = 4096;        // pairs per level-1 block (kBlock threads x 16)
 constexpr int kMaxBuckets = 4096;
 constexpr int kMaxRbShift = 12;       // rows per bucket <= 4096 (level-2 LDS histogram)
+// Pairs per level-1 bucket (at most; the bound is the raw edge count): 32768
+// with a 1024-thread level-2 block -- config3's CSR 0.54 -> 0.44 ms against 8192
+// with 256 threads (longer runs per bucket in the level-1 scatter, fewer
+// level-1 counters to zero; rows-per-bucket sweep in
+// profiles/r04/build4/csr_bucket_sweep.txt).
+constexpr double kBucketPairs = 32768.0;
+constexpr int kRowsBlock = 1024;
 
 __global__ __launch_bounds__(kBlock) void k_bucket_hist(const int32_t* __restrict__ rows,
                                                         int64_t cap, const int64_t* n_dev,
@@ -222,10 +229,12 @@ __global__ __launch_bounds__(kBlock) void k_bucket_scatter(
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_bucket_rows(
+template <int BT>
+__global__ __launch_bounds__(BT) void k_bucket_rows(
     const int32_t* __restrict__ trow, const int32_t* __restrict__ tcol, int rb, int64_t n_rows,
     int64_t n_blocks, const int64_t* __restrict__ Hoff, int64_t* __restrict__ seg_ptr,
     int32_t* __restrict__ seg) {
+  constexpr int kBlock = BT, kWavesPerBlock = BT / kWave;
   __shared__ uint32_t cnt[1 << kMaxRbShift];
   __shared__ uint32_t wsum[kWavesPerBlock];
   const int64_t b = blockIdx.x;
@@ -280,7 +289,7 @@ BucketPlan bucket_plan(int64_t cap, int64_t n_rows) {
   BucketPlan P{false, 0, 0, 0};
   if (cap <= 0 || n_rows <= 0) return P;
   int rb = 0;
-  while (rb < kMaxRbShift && (static_cast<double>(cap) * (1ll << (rb + 1))) / n_rows <= 8192.0) ++rb;
+  while (rb < kMaxRbShift && (static_cast<double>(cap) * (1ll << (rb + 1))) / n_rows <= kBucketPairs) ++rb;
   while (rb < kMaxRbShift && ((n_rows + (1ll << rb) - 1) >> rb) > kMaxBuckets) ++rb;
   const int64_t nbk = (n_rows + (1ll << rb) - 1) >> rb;
   if (nbk > kMaxBuckets) return P;
@@ -1263,7 +1272,7 @@ int dps_csr_build(const int32_t* rows, const int32_t* cols, int64_t n_pairs,
     k_bucket_scatter<<<static_cast<unsigned>(B.n_blocks), kBlock, 0, st>>>(
         rows, cols, n_pairs, n_pairs_dev, B.rb, B.n_buckets, B.n_blocks, Hoff, trow, tcol);
     DPS_LAUNCHED();
-    k_bucket_rows<<<static_cast<unsigned>(B.n_buckets), kBlock, 0, st>>>(
+    k_bucket_rows<kRowsBlock><<<static_cast<unsigned>(B.n_buckets), kRowsBlock, 0, st>>>(
         trow, tcol, B.rb, n_rows, B.n_blocks, Hoff, seg_ptr, tmp);
     DPS_LAUNCHED();
   } else {
