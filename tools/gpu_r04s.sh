@@ -28,6 +28,11 @@ if [ -n "${PMC:-}" ]; then
   tools/pmc_hot.sh || exit 1
   mv gpurun_out/pmc_hot.json $O/ && mkdir -p $O/pmc && mv gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_valu gpurun_out/pmc_lds $O/pmc/
 fi
+if [ -n "${SHARD:-}" ]; then
+  timeout -k 10 300 python3 -u tools/shard_balance.py > $O/shard_balance.txt 2>&1 \
+    || { echo "shard_balance failed"; tail -20 $O/shard_balance.txt; exit 1; }
+  grep -v amdgpu.ids $O/shard_balance.txt
+fi
 if [ -n "${PHASES:-}" ]; then
   DPATHSIM_LIB=$PWD/distributed-pathsim_amd/dpathsim/libdpathsim_prof.so timeout -k 10 300 \
     python3 -u tools/lean_phases.py > $O/lean_phases.txt 2>&1 || { echo "phases failed"; tail -20 $O/lean_phases.txt; exit 1; }
