@@ -902,16 +902,27 @@ __global__ __launch_bounds__(kBlock) void k_expand(const int64_t* __restrict__ a
       const int o = wave_owner(a.excl, i);
       const int64_t bo = readlane_var(a.b, o);
       const uint32_t eo = static_cast<uint32_t>(__shfl(static_cast<int>(a.excl), o, kWave));
-      int64_t pb = 0, pl = 0;
+      int64_t pb = 0;
+      uint32_t pl = 0;
       if (i < a.total) {
         const int32_t p = ap_col[bo + (i - eo)];
         pb = px_ptr[p];
-        pl = px_ptr[p + 1] - pb;
+        pl = static_cast<uint32_t>(px_ptr[p + 1] - pb);
       }
-      const int64_t inc = wave_inclusive_sum(pl);
-      const int64_t w = carry + inc - pl;
-      for (int64_t t = 0; t < pl; ++t) tmp[w + t] = px_col[pb + t];
-      carry += readlane(inc, kWave - 1);
+      // the strip's mids, 64 at a time: each lane copies one (its paper by a
+      // second owner search), so the loads of a strip are all in flight at
+      // once instead of one paper's mids one after another per lane
+      const uint32_t inc = wave_inclusive_sum(pl);
+      const uint32_t pex = inc - pl;
+      const uint32_t tot = readlane(inc, kWave - 1);
+      for (uint32_t m0 = 0; m0 < tot; m0 += kWave) {
+        const uint32_t m = m0 + static_cast<uint32_t>(lane);
+        const int po = wave_owner(pex, m);
+        const int64_t pbo = readlane_var(pb, po);
+        const uint32_t peo = static_cast<uint32_t>(__shfl(static_cast<int>(pex), po, kWave));
+        if (m < tot) tmp[carry + m] = px_col[pbo + (m - peo)];
+      }
+      carry += tot;
     }
   }
 }
