@@ -232,3 +232,49 @@ def test_split_rows_identical(M, P, k):
         for a, b in zip(got, whole):
             assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
                                   (b.view(np.int64) if b.dtype == np.float64 else b)[r0:r1])
+
+
+@pytest.mark.parametrize("nv,multi", [(400, 1), (9000, 1), (9000, 3)])
+def test_segment_length_classes(nv, multi):
+    """Rows whose lengths sit on every boundary of the segmented sort + unique
+    (lane networks <= 16 / <= 32, wave <= 64, wave LDS bitonic <= 256, block
+    rank sort <= 1024, LDS bitonic <= 14336, in-place global sort above), with
+    duplicate authorships (the typed CSR's distinct) and 1 or up to 3 venues
+    per paper (the single-mid gather path with and without the LDS histogram,
+    and the expansion path): C, s, g and the top-k against the oracle."""
+    import pathsim_oracle as po
+    from dpathsim.engine import build_engine
+    from dpathsim.graph import Graph
+    rng = np.random.default_rng(nv + multi)
+    lengths = [2, 16, 17, 32, 33, 64, 65, 256, 257, 1024, 1025, 14336, 14337, 15000]
+    papers_of = lengths + [1] * 300
+    na = len(papers_of)
+    n_pap = sum(papers_of)
+    src, dst = [], []
+    pid = 0
+    for a, n in enumerate(papers_of):
+        for _ in range(n):
+            src.append(a), dst.append(na + pid)
+            pid += 1
+    for _ in range(500):                      # duplicate authorships
+        i = int(rng.integers(0, len(src)))
+        src.append(src[i]), dst.append(dst[i])
+    n_ap = len(src)
+    for p in range(n_pap):
+        for _ in range(int(rng.integers(1, multi + 1))):
+            src.append(na + p), dst.append(na + n_pap + int(rng.integers(0, nv)))
+    types = np.concatenate([np.zeros(na), np.ones(n_pap), np.full(nv, 2)]).astype(np.int32)
+    rel = np.concatenate([np.zeros(n_ap), np.ones(len(src) - n_ap)]).astype(np.int32)
+    g = Graph(types, ["author", "paper", "venue"], np.array(src), np.array(dst), rel,
+              ["author_of", "submit_at"], node_ids=lambda i: f"n{i}", labels=lambda i: f"L{i}")
+    t = g.typed()
+    eng = build_engine(t, tile_w=1024)
+    co = po.COracle.from_typed(t)
+    cp, cc, cv, s, gg = co.export()
+    nnz = eng.info.nnz_c
+    assert np.array_equal(eng.tensor("c_ptr")[: na + 1].cpu().numpy(), cp)
+    assert np.array_equal(eng.tensor("c_col")[:nnz].cpu().numpy(), cc)
+    assert np.array_equal(eng.tensor("c_val")[:nnz].cpu().numpy(), cv)
+    assert np.array_equal(eng.tensor("s")[:nv].cpu().numpy(), s)
+    assert np.array_equal(eng.tensor("g")[:na].cpu().numpy(), gg)
+    _same([a.cpu().numpy() for a in eng.topk(10)], co.topk(10, 0, na))
