@@ -829,10 +829,19 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
 #endif
 constexpr int kSel = DPS_KSEL;
 
+// The wave raises its issue priority while it computes and issues a batch of
+// chunk loads and drops it after (s_setprio 1 / 0): the SIMD's arbiter then
+// favours a wave that is about to put loads in flight over waves in their
+// scatter or epilogue, so more loads overlap -- config3 k_cct1 66.2-66.3 ms
+// against 67.1 ms at priority 0, the same output (profiles/r04/exp/ab_prio.txt;
+// priority 3 the same as 1).
+#ifndef DPS_PRIO_ISSUE
+#define DPS_PRIO_ISSUE 1
+#endif
 __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __restrict__ ent,
                                        int lane, Batch& B) {
-#ifdef DPS_PRIO_ISSUE
-  __builtin_amdgcn_s_setprio(DPS_PRIO_ISSUE);   // experiment: loads out first
+#if DPS_PRIO_ISSUE
+  __builtin_amdgcn_s_setprio(DPS_PRIO_ISSUE);
 #endif
   const bool vl = lane < S.G.nv;
 #pragma unroll
@@ -867,7 +876,7 @@ __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __
     B.e[u] = *reinterpret_cast<const uint4*>(ent + (live ? bj + 4u * static_cast<uint32_t>(q) : 0u));
     B.c[u] = live ? cj : 0;
   }
-#ifdef DPS_PRIO_ISSUE
+#if DPS_PRIO_ISSUE
   __builtin_amdgcn_s_setprio(0);
 #endif
 }
