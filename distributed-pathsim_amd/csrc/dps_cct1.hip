@@ -46,6 +46,7 @@
 #include "dps_cct_dev.hpp"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dps {
 namespace {
@@ -921,6 +922,12 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
 // OPT: the optimistic 4-bit passes compiled in (launched only with tile_sum:
 // the instantiation without them keeps the old register allocation -- the
 // redo queue and the check alone cost 3 ms of the non-optimistic launch).
+// kcold() reads CctParams fields from the kernarg segment at their offsetof:
+// valid only while the by-value CctParams is k_cct1's FIRST and ONLY argument
+// (kernarg offset 0) and only in code inlined into k_cct1 (win_ub,
+// extra_groups and the row loop).  Do not add a kernel argument or call a
+// kcold-using helper from another kernel.
+static_assert(std::is_trivially_copyable<CctParams>::value, "CctParams is passed by value");
 template <int F, int KPL, bool HV, bool SY, bool OPT>
 // The symmetric-mode instantiation carries the record path and the published
 // bounds: DPS_SYM_WPE waves per SIMD (4: 128 VGPRs, no spills).
@@ -1239,6 +1246,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
               const uint32_t ua = (bad & 1u) ? S_hb & 0xFFFFu : 0u;
               const uint32_t ubb = (bad & 2u) && tb < p.T8 ? S_hb >> 16 : 0u;
               auto push = [&](int t8, uint32_t u) {
+                DPS_DASSERT(rq_n < 4);   // the bound argued at rq's declaration
                 const uint32_t e = (static_cast<uint32_t>(t8) << 8) | u;
                 if (rq_n == 0) rq[0] = e;
                 else if (rq_n == 1) rq[1] = e;

@@ -88,19 +88,23 @@ __global__ __launch_bounds__(kBlock) void k_pack_counts(const int32_t* __restric
 // with edges[r] <= x < edges[r+1], at gathered row r * m + (x - edges[r]).
 __global__ __launch_bounds__(kBlock) void k_unpack_gathered(const int64_t* __restrict__ gathered,
                                                             int world, int64_t m, int k,
+                                                            int64_t n_rows,
                                                             const int64_t* __restrict__ edges,
                                                             const int64_t* __restrict__ den,
                                                             int32_t* __restrict__ out_idx,
                                                             int64_t* __restrict__ out_cnt,
                                                             double* __restrict__ out_score) {
   const int64_t x0 = edges[0];
-  const int64_t n = (edges[world] - x0) * k;
+  // the out_* arrays hold n_rows rows: never more, whatever the device edges say
+  const int64_t span = edges[world] - x0;
+  const int64_t n = (span < n_rows ? span : n_rows) * k;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * kBlock) {
     const int64_t x = x0 + i / k;
     const int s = static_cast<int>(i % k);
     int r = 0;
     while (r + 1 < world && edges[r + 1] <= x) ++r;
+    if (x - edges[r] >= m) continue;   // a shard longer than the gathered block: not sent
     const uint64_t w = static_cast<uint64_t>(gathered[(r * m + (x - edges[r])) * k + s]);
     const int32_t y = static_cast<int32_t>(static_cast<uint32_t>(w));
     const int64_t c = static_cast<int64_t>(w >> 32);
@@ -170,7 +174,7 @@ int dps_unpack_gathered(const int64_t* gathered, int32_t world, int64_t m, int32
   DPS_REQUIRE(gathered && edges && den && out_idx && out_cnt && out_score, DPS_ERR_INVALID,
               "null array");
   k_unpack_gathered<<<grid_for(n_rows * k, kBlock), kBlock, 0, static_cast<hipStream_t>(stream)>>>(
-      gathered, world, m, k, edges, den, out_idx, out_cnt, out_score);
+      gathered, world, m, k, n_rows, edges, den, out_idx, out_cnt, out_score);
   DPS_LAUNCHED();
   return DPS_OK;
 }

@@ -917,7 +917,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_keys(const int64_t* __restrict_
                                                       const int32_t* __restrict__ c_val,
                                                       const int32_t* __restrict__ rank,
                                                       const int64_t* __restrict__ Q,
-                                                      int64_t n_rows, int shift,
+                                                      int64_t n_rows, int shift, int64_t cap,
                                                       uint64_t* __restrict__ keys,
                                                       uint32_t* __restrict__ vals,
                                                       int32_t* __restrict__ status) {
@@ -952,8 +952,10 @@ __global__ __launch_bounds__(kBlock) void k_tile_keys(const int64_t* __restrict_
           c = 0xFFFFu;
         }
         const int64_t d = static_cast<int64_t>(qk + i);
-        keys[d] = (static_cast<uint64_t>(lb >> shift) << 32) | v;
-        vals[d] = ((lb & ymask) << 16) | c;
+        if (d < cap) {   // past an undersized nnz_cap: k_tile_keys_pad reports the overflow
+          keys[d] = (static_cast<uint64_t>(lb >> shift) << 32) | v;
+          vals[d] = ((lb & ymask) << 16) | c;
+        }
       }
     }
   }
@@ -984,8 +986,11 @@ __global__ __launch_bounds__(kBlock) void k_tile_gmin(const int32_t* __restrict_
 __global__ __launch_bounds__(kBlock) void k_tile_keys_pad(const int64_t* __restrict__ c_ptr,
                                                           int64_t n_rows, int64_t cap, uint64_t pad,
                                                           uint64_t* __restrict__ keys,
-                                                          uint32_t* __restrict__ vals) {
+                                                          uint32_t* __restrict__ vals,
+                                                          int32_t* __restrict__ status) {
   const int64_t nnz = c_ptr[n_rows] - c_ptr[0];
+  // the caller's nnz_cap is a host bound; C's real size is only known here
+  if (nnz > cap && blockIdx.x == 0 && threadIdx.x == 0 && status) *status = DPS_ERR_OVERFLOW;
   for (int64_t i = nnz + static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < cap;
        i += static_cast<int64_t>(gridDim.x) * kBlock) {
     keys[i] = pad;
@@ -1377,7 +1382,7 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
     DPS_LAUNCHED();
     DPS_HIP_RET(scan_exclusive<uint32_t>(len, Q, n_targets, sws_q, scan_q, st));
     k_tile_keys<<<grid_for((n_targets + kWave - 1) / kWave * kWave, kBlock, 4096), kBlock, 0, st>>>(
-        c_ptr, c_col, c_val, t_rank, Q, n_targets, shift, keys, vals, status_dev);
+        c_ptr, c_col, c_val, t_rank, Q, n_targets, shift, cap, keys, vals, status_dev);
     DPS_LAUNCHED();
     if (tile_gmin) {
       k_tile_gmin<<<static_cast<unsigned>(T), kBlock, 0, st>>>(perm, g, n_targets, shift, tile_gmin);
@@ -1385,7 +1390,8 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
     }
   }
   k_tile_keys_pad<<<grid_for(cap, kBlock), kBlock, 0, st>>>(c_ptr, n_targets, cap,
-                                                           static_cast<uint64_t>(n_mids), keys, vals);
+                                                           static_cast<uint64_t>(n_mids), keys, vals,
+                                                           status_dev);
   DPS_LAUNCHED();
   int key_bits = 1;
   while ((int64_t(1) << key_bits) <= n_mids) ++key_bits;   // n_mids itself is the pad mid

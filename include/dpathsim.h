@@ -290,7 +290,9 @@ size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t ti
  * are laid out from ONE stable radix sort of (bucket, entry) pairs instead of
  * per-entry global atomics on n_mids*T bucket counters (config4, 200 k
  * topics); otherwise identical to dps_ct_tiles_build.  Same outputs and
- * format; ws from dps_ct_tiles_workspace_size2. */
+ * format; ws from dps_ct_tiles_workspace_size2.  A bound below the real nnz is
+ * detected on the device: *status_dev = DPS_ERR_OVERFLOW, the outputs are then
+ * undefined and nothing is written past the workspace. */
 size_t dps_ct_tiles_workspace_size2(int64_t n_mids, int64_t n_targets, int32_t tile_w,
                                     int64_t nnz_cap);
 int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
@@ -533,7 +535,9 @@ int dps_pair_count(const int32_t* a_col, const int32_t* a_val, int64_t a_len,
  *   x - edges[r]: out_idx / out_cnt [n_rows, k] and out_score = double(2 cnt) /
  *   double(den[x] + den[idx]) -- the hot kernel's division of the same exact
  *   integers (:51-52), bit-identical -- 0.0 for empty (-1) or zero-count slots.
- *   n_rows must equal edges[world] - edges[0].
+ *   n_rows must equal edges[world] - edges[0]; the kernel never writes past
+ *   n_rows rows nor reads past a shard's m gathered rows if the device edges
+ *   disagree (those slots are then left unwritten).
  * ------------------------------------------------------------------------- */
 size_t dps_shard_edges_workspace_size(int64_t n_rows);
 int dps_shard_edges(const int64_t* terms, int64_t n_rows, int32_t world, int64_t* edges,

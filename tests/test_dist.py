@@ -145,8 +145,16 @@ def test_shard_edges_host_equals_row_work_plan(world):
     mism = torch.zeros(1, dtype=torch.int64)
     shard_edges(terms, world, ref=ref, mismatch=mism)
     assert int(mism) == 0
-    shard_edges(terms + 7 * (torch.arange(terms.numel()) % 3 == 0), world, ref=ref, mismatch=mism)
-    assert world == 1 or int(mism) >= 0
+    pert = terms + 7 * (torch.arange(terms.numel()) % 3 == 0)
+    want = int((shard_edges(pert, world) != ref).sum())
+    shard_edges(pert, world, ref=ref, mismatch=mism)
+    assert int(mism) == want
+    if world > 1:                       # a reference plan off by one edge: exactly one mismatch
+        bad = ref.clone()
+        bad[1] += 1
+        mism.zero_()
+        shard_edges(terms, world, ref=bad, mismatch=mism)
+        assert int(mism) == 1
     assert shard_edges(torch.zeros(0, dtype=torch.int64), world).tolist() == [0] * (world + 1)
 
 
