@@ -65,7 +65,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dpathsim.dist import RcclComm, gather_topk_compact, max_shard, pack_counts, shard_edges
+    from dpathsim.dist import (RcclComm, TileSplit, gather_topk_compact, max_shard, pack_counts,
+                               shard_edges)
     from dpathsim.engine import PathSimEngine
     from dpathsim.synth import CONFIGS, synth_config
 
@@ -103,9 +104,16 @@ def main():
     args.tile_w = eng.tile_w
     if args.venue_skip is not None:
         eng.venue_skip = bool(args.venue_skip) and args.denominator == "rowsum"
+    # N > 1: each rank builds the C^T tiles of its own target-tile range and the
+    # slices are all-gathered (dist.TileSplit); C, g and the
+    # target order stay replicated.  DPATHSIM_BENCH_SPLIT=0: every rank builds
+    # every tile (the round-4 build).
+    if world > 1 and os.environ.get("DPATHSIM_BENCH_SPLIT", "1") == "1":
+        eng.split = TileSplit.from_group(comm=comm, device=dev)
     eng.upload()
 
-    eng.build()             # checks the overflow conditions once (one sync)
+    eng.build()             # checks the overflow conditions once (one sync); with the
+                            # tile split also the gather plan (one collective)
     # contiguous row shards of equal estimated work (dps_shard_edges over the
     # build's row work; every rank derives the same edges from its own,
     # identical C: no communication), read back once, outside the timed loop
@@ -281,10 +289,26 @@ def main():
         h2d.append((time.perf_counter() - t1) * 1e3)
         del held
     h2d_ms = float(np.median(h2d))
+    # the same copies from pinned (page-locked) host buffers, as a caller that
+    # stages its edge list for the GPU would hand them over
+    pinned = [torch.from_numpy(np.ascontiguousarray(a)).pin_memory() for a in h2d_arrays]
+    h2d_p = []
+    for _ in range(3):
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        held = [a.to(dev, non_blocking=True) for a in pinned]
+        torch.cuda.synchronize(dev)
+        h2d_p.append((time.perf_counter() - t1) * 1e3)
+        del held
+    del pinned
+    h2d_pin_ms = float(np.median(h2d_p))
     pcie = {"h2d_bytes": h2d_bytes, "h2d_ms": h2d_ms, "h2d_GBps": h2d_bytes / (h2d_ms * 1e-3) / 1e9,
             "value_incl_h2d": pairs / ((ms_per_step + h2d_ms) * 1e-3),
-            "note": "edge list + node tables copied from pageable host memory each step; "
-                    "not the reported value (inputs resident in HBM)"}
+            "h2d_pinned_ms": h2d_pin_ms,
+            "h2d_pinned_GBps": h2d_bytes / (h2d_pin_ms * 1e-3) / 1e9,
+            "value_incl_h2d_pinned": pairs / ((ms_per_step + h2d_pin_ms) * 1e-3),
+            "note": "SURVEY 8d's host-resident variant: the edge list + node tables copied "
+                    "host -> HBM each step (pageable, and pinned); not the reported value"}
 
     # ---- CPU baseline: the oracle's C port on a bounded row sample ----------
     cpu = None
@@ -333,7 +357,12 @@ def main():
                                    f"{typed.n_mids} {typed.metapath.mid_type}s, all-pairs top-{k}",
                        "n_authors": NA, "k": k, "tile_w": args.tile_w,
                        "nnz_C": info.nnz_c, "sum_terms": terms if world == 1 else None,
-                       "parallelism": f"row-shard x{world} (work-balanced, heaviest rows first)"},
+                       "inputs": "edge list + node tables resident in HBM when the timed "
+                                 "region starts (the bench contract); SURVEY 8d times them "
+                                 "host-resident: that rate is pcie_inclusive.value_incl_h2d*",
+                       "parallelism": f"row-shard x{world} (work-balanced, heaviest rows first)",
+                       "build": ("C^T tiles split by target-tile range + all-gather"
+                                 if eng.split is not None else "replicated")},
             # bound: the LDS array (the resource the algorithm's unit work lands on;
             # the kernel itself is issue/latency-bound at the occupancy its LDS
             # allows)

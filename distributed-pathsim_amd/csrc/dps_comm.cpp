@@ -4,7 +4,8 @@
 // gloo carries the 128 bytes; no tensor data goes through PyTorch).  The
 // collectives replace the Spark shuffle that brings per-target counts back to
 // the driver (DPathSim_APVPA.py:86,107 -- .count() -- and :146-168): a gather
-// of every rank's finished top-k block to the root, and a broadcast.
+// of every rank's finished top-k block to the root, a broadcast, and the
+// all-gather of the ranks' C^T tile slices (N > 1 build).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -65,6 +66,14 @@ int dps_gather(void* comm, const void* send, void* recv, size_t bytes, int32_t r
   return nccl_ret(ncclGather(send, recv, bytes, ncclUint8, root, static_cast<ncclComm_t>(comm),
                              static_cast<hipStream_t>(stream)),
                   "ncclGather");
+}
+
+int dps_allgather(void* comm, const void* send, void* recv, size_t bytes, void* stream) {
+  DPS_REQUIRE(comm, DPS_ERR_INVALID, "null comm");
+  DPS_REQUIRE((send && recv) || bytes == 0, DPS_ERR_INVALID, "null buffer");
+  return nccl_ret(ncclAllGather(send, recv, bytes, ncclUint8, static_cast<ncclComm_t>(comm),
+                                static_cast<hipStream_t>(stream)),
+                  "ncclAllGather");
 }
 
 }  // extern "C"

@@ -103,11 +103,19 @@ SIGNATURES = {
     "dps_comm_destroy": (C.c_int, [_p]),
     "dps_bcast": (C.c_int, [_p, _p, _sz, _i32, _p]),
     "dps_gather": (C.c_int, [_p, _p, _p, _sz, _i32, _p]),
+    "dps_allgather": (C.c_int, [_p, _p, _p, _sz, _p]),
     "dps_get_tuning": (C.c_int, [_i32]),
     "dps_shard_edges_workspace_size": (_sz, [_i64]),
     "dps_shard_edges": (C.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "dps_pack_counts": (C.c_int, [_p, _p, _i64, _p, _p]),
     "dps_unpack_gathered": (C.c_int, [_p, _i32, _i64, _i32, _p, _i64, _p, _p, _p, _p, _p]),
+    "dps_label_rows_workspace_size": (_sz, [_i64]),
+    "dps_label_rows": (C.c_int, [_p, _p, _p, _p, _i64, _i64, _p, _p, _p, _p, _sz, _p]),
+    "dps_tiles_slice_words": (_i64, [_i64, _i64, _i64]),
+    "dps_tiles_pack": (C.c_int, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _p, _p]),
+    "dps_tiles_assemble_workspace_size": (_sz, [_i64, _i32]),
+    "dps_tiles_assemble": (C.c_int, [_p, _i32, _i64, _i64, _i64, _i64, _p, _p, _i64, _p, _p, _p,
+                                     _p, _sz, _p]),
     "dps_topk_merge": (C.c_int, [_p, _p, _p, _p, _i64, _i32, _i32, _i64, _i64, _p, _p, _p, _p]),
     "dps_heavy_first_workspace_size": (_sz, [_i64]),
     "dps_heavy_first": (C.c_int, [_p, _i64, _i64, _i64, _i32, _p, _p, _sz, _p]),

@@ -73,6 +73,18 @@ class RcclComm:
                            recv.data_ptr() if recv is not None else None, nb, root, self._stream())
         return recv
 
+    def allgather(self, send: torch.Tensor, recv: torch.Tensor):
+        """Every rank's ``send`` bytes into ``recv`` on every rank (rank r at
+        byte offset r * send.nbytes); device tensors, current stream."""
+        send = send.contiguous()
+        nb = send.numel() * send.element_size()
+        if recv.numel() * recv.element_size() < self.world * nb:
+            raise ValueError("receive buffer smaller than world * send bytes")
+        with torch.cuda.device(self.device):
+            self._lib.call("dps_allgather", self._h, send.data_ptr(), recv.data_ptr(), nb,
+                           self._stream())
+        return recv
+
     def bcast(self, buf: torch.Tensor, root: int = 0):
         with torch.cuda.device(self.device):
             self._lib.call("dps_bcast", self._h, buf.data_ptr(), buf.numel() * buf.element_size(),
@@ -89,6 +101,52 @@ class RcclComm:
             self.close()
         except Exception:
             pass
+
+
+class TileSplit:
+    """The N > 1 build's tile split (PathSimEngine.split): rank r builds the C^T
+    tiles of its own target-tile range (dps_label_rows + dps_ct_tiles_build2
+    over that sub-C), the ranks all-gather the slices, and every rank assembles
+    the full layout (dps_tiles_assemble).  ``allgather(send, recv)`` is a
+    collective on the current stream (RCCL through :class:`RcclComm` or the
+    nccl process group; over gloo the bytes go through host memory), and
+    ``allreduce_max(int)`` a host-value collective for the plan.  ``caps`` --
+    tile width -> slice entry capacity -- is the plan every later build of the
+    same graph gathers with (PathSimEngine.check sets it after the first)."""
+
+    def __init__(self, rank: int, world: int, allgather, allreduce_max):
+        if world < 1 or not 0 <= rank < world:
+            raise ValueError(f"bad rank {rank} / world {world}")
+        self.rank, self.world = rank, world
+        self.allgather = allgather
+        self.allreduce_max = allreduce_max
+        self.caps = {}
+
+    @classmethod
+    def from_group(cls, group=None, comm: "RcclComm | None" = None, device=None):
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        nccl = dist.get_backend(group) == "nccl"
+        dev = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+
+        if comm is not None:
+            def ag(send, recv):
+                comm.allgather(send, recv)
+        elif nccl:
+            def ag(send, recv):
+                dist.all_gather_into_tensor(recv, send, group=group)
+        else:
+            def ag(send, recv):          # gloo (CPU rehearsals): through host memory
+                parts = [torch.empty_like(send, device="cpu") for _ in range(world)]
+                dist.all_gather(parts, send.cpu(), group=group)
+                recv.copy_(torch.cat(parts).to(recv.device))
+
+        def amax(v: int) -> int:
+            t = torch.tensor([int(v)], dtype=torch.int64, device=dev if nccl else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            return int(t.item())
+
+        return cls(rank, world, ag, amax)
 
 
 def shard_bounds(n_rows: int, rank: int, world: int) -> tuple[int, int]:

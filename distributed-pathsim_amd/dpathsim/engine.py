@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from ._lib import DPS_ERR_OVERFLOW
 from .graph import TypedTables
 
 # one tile of 16384 targets per wave: 4-bit counters in 8 KiB of LDS (a tile
@@ -124,6 +125,10 @@ class PathSimEngine:
         # launch are cut into `pieces` target-tile ranges (see topk())
         self.split_rows = DEFAULT_SPLIT_ROWS
         self.pieces = DEFAULT_PIECES
+        # N > 1 (dist.TileSplit): this rank builds the C^T tiles of its own
+        # target-tile range only and the ranks all-gather the slices
+        self.split = None
+        self._split_state = {}
         self.info = BuildInfo()
         self.built = False
         self.checked = False
@@ -284,39 +289,53 @@ class PathSimEngine:
                       _ptr(t_rank), _ptr(g_t), _ptr(ows), ows.numel(), st)
             del ows
             mark("order")
+            split = self.split if self.split is not None and self.split.world > 1 else None
+            self._split_state = {}
             T = max(1, math.ceil(NA / self.tile_w)) if NA else 1
-            tile_off = self._empty(NV * T + 1, torch.int32)
-            tile_maxc = self._empty(NV * T + 1, torch.int32)
-            tile_gmin = self._empty(T, torch.int64)
             ent_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV, NA,
                                 self.tile_w)
             if ent_cap >= 2 ** 32:
                 raise OverflowError("padded nnz(C) >= 2^32 exceeds the uint32 tile offsets")
-            tile_ent = self._empty(ent_cap, torch.int32)
-            status = self._empty(1, torch.int32)
-            # (many mids: laid out from one radix sort of (bucket, entry) pairs,
-            # dps_ct_tiles_build2; bnd.expand bounds nnz over the author rows)
-            tws = self._ws(_lib.size("dps_ct_tiles_workspace_size2", NV, NA, self.tile_w, bnd.expand))
-            _lib.call("dps_ct_tiles_build2", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(den),
-                      _ptr(t_rank), NA, NV, self.tile_w, bnd.expand, _ptr(tile_off), _ptr(tile_ent),
-                      _ptr(tile_maxc), _ptr(tile_gmin), _ptr(status), _ptr(tws), tws.numel(), st)
+            sub = self._label_rows(split, c_ptr, c_col, c_val, t_perm) if split else None
+            if split:
+                tile_off, tile_ent, tile_maxc, tile_gmin, status = self._split_tiles(
+                    split, sub, self.tile_w, g_t, True, ent_cap)
+            else:
+                tile_off = self._empty(NV * T + 1, torch.int32)
+                tile_maxc = self._empty(NV * T + 1, torch.int32)
+                tile_gmin = self._empty(T, torch.int64)
+                tile_ent = self._empty(ent_cap, torch.int32)
+                status = self._empty(1, torch.int32)
+                # (many mids: laid out from one radix sort of (bucket, entry) pairs,
+                # dps_ct_tiles_build2; bnd.expand bounds nnz over the author rows)
+                tws = self._ws(_lib.size("dps_ct_tiles_workspace_size2", NV, NA, self.tile_w,
+                                         bnd.expand))
+                _lib.call("dps_ct_tiles_build2", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(den),
+                          _ptr(t_rank), NA, NV, self.tile_w, bnd.expand, _ptr(tile_off),
+                          _ptr(tile_ent), _ptr(tile_maxc), _ptr(tile_gmin), _ptr(status), _ptr(tws),
+                          tws.numel(), st)
+                del tws
             mark("tiles")
-            del tws
             half = None
             if self.tile_w == 16384 and self.half_tiles:
                 # companion u8 tiles at 8192: a tile whose 4-bit bound exceeds 15
                 # runs as its two halves from these (dps_cct_ext)
                 T8 = max(1, math.ceil(NA / 8192)) if NA else 1
-                h_off = self._empty(NV * T8 + 1, torch.int32)
-                h_maxc = self._empty(NV * T8 + 1, torch.int32)
                 h_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV, NA, 8192)
-                h_ent = self._empty(h_cap, torch.int32)
-                h_status = self._empty(1, torch.int32)
-                hws = self._ws(_lib.size("dps_ct_tiles_workspace_size2", NV, NA, 8192, bnd.expand))
-                _lib.call("dps_ct_tiles_build2", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), None,
-                          _ptr(t_rank), NA, NV, 8192, bnd.expand, _ptr(h_off), _ptr(h_ent),
-                          _ptr(h_maxc), None, _ptr(h_status), _ptr(hws), hws.numel(), st)
-                del hws
+                if split:
+                    h_off, h_ent, h_maxc, _, h_status = self._split_tiles(split, sub, 8192, g_t,
+                                                                          False, h_cap)
+                else:
+                    h_off = self._empty(NV * T8 + 1, torch.int32)
+                    h_maxc = self._empty(NV * T8 + 1, torch.int32)
+                    h_ent = self._empty(h_cap, torch.int32)
+                    h_status = self._empty(1, torch.int32)
+                    hws = self._ws(_lib.size("dps_ct_tiles_workspace_size2", NV, NA, 8192,
+                                             bnd.expand))
+                    _lib.call("dps_ct_tiles_build2", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), None,
+                              _ptr(t_rank), NA, NV, 8192, bnd.expand, _ptr(h_off), _ptr(h_ent),
+                              _ptr(h_maxc), None, _ptr(h_status), _ptr(hws), hws.numel(), st)
+                    del hws
                 # per-bucket count sums of the companion tiles: the hot kernel's
                 # optimistic 4-bit passes check each half's digit sum against
                 # them (dps_cct_ext.tile_sum)
@@ -327,6 +346,7 @@ class PathSimEngine:
                               _ptr(t_sum), st)
                 half = (h_off, h_ent, h_maxc, h_status, t_sum)
                 mark("half_tiles")
+            del sub
             hv_slot = hv_c = None
             if self.venue_skip and self.denominator == "rowsum" and NA and NV:
                 # venue skipping: the heavy venues (most author entries) and the
@@ -364,6 +384,87 @@ class PathSimEngine:
             self.check()
         return self
 
+    # ------------------------------------------------- N > 1 tile slices
+    def _split_range(self, split):
+        """This rank's target labels [l0, l1): tiles_per_rank tiles of tile_w
+        (the same count on every rank, the last ranks may hold fewer)."""
+        NA = self.typed.n_authors
+        T = max(1, math.ceil(NA / self.tile_w)) if NA else 1
+        tr = -(-T // split.world)
+        l0 = min(NA, split.rank * tr * self.tile_w)
+        return l0, min(NA, l0 + tr * self.tile_w), tr
+
+    def _label_rows(self, split, c_ptr, c_col, c_val, t_perm):
+        """Sub-C of this rank's labels in label order (dps_label_rows)."""
+        l0, l1, _ = self._split_range(split)
+        n = l1 - l0
+        cap = self.bounds.expand
+        sub_ptr = self._empty(n + 1, torch.int64)
+        sub_col, sub_val = self._empty(cap, torch.int32), self._empty(cap, torch.int32)
+        ws = self._ws(_lib.size("dps_label_rows_workspace_size", n))
+        _lib.call("dps_label_rows", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(t_perm), l0, l1,
+                  _ptr(sub_ptr), _ptr(sub_col), _ptr(sub_val), _ptr(ws), ws.numel(), self.stream)
+        return (l0, l1, sub_ptr, sub_col, sub_val)
+
+    def _split_tiles(self, split, sub, W, g_t, gmin, ent_cap):
+        """Tiles of width W over this rank's labels (dps_ct_tiles_build2 on the
+        sub-C), packed into a slice (dps_tiles_pack), all-gathered, assembled
+        into the full layout (dps_tiles_assemble).  The slice's entry capacity
+        is the plan in split.caps[W] (the largest slice of an earlier build of
+        the same graph, see check()) or, before one exists, the host bound."""
+        l0, l1, sub_ptr, sub_col, sub_val = sub
+        NA, NV = self.typed.n_authors, self.typed.n_mids
+        st = self.stream
+        bnd = self.bounds
+        _, _, tr_unit = self._split_range(split)
+        tr = tr_unit * (self.tile_w // W)
+        T = max(1, math.ceil(NA / W)) if NA else 1
+        n = l1 - l0
+        tl = -(-n // W)
+        # (the host bound over the largest range, the same on every rank: the
+        # gathered slices must all have one size)
+        loc_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV,
+                            tr_unit * self.tile_w, W)
+        loc_off = self._empty(NV * tl + 1, torch.int32)
+        loc_maxc = self._empty(NV * tl + 1, torch.int32)
+        loc_gmin = self._empty(tl, torch.int64) if gmin else None
+        loc_ent = self._empty(loc_cap + 4, torch.int32)
+        status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if n > 0:
+            ws = self._ws(_lib.size("dps_ct_tiles_workspace_size2", NV, n, W, bnd.expand))
+            g_ptr = g_t.data_ptr() + 8 * l0 if gmin else None
+            _lib.call("dps_ct_tiles_build2", _ptr(sub_ptr), _ptr(sub_col), _ptr(sub_val), g_ptr,
+                      None, n, NV, W, bnd.expand, _ptr(loc_off), _ptr(loc_ent), _ptr(loc_maxc),
+                      _ptr(loc_gmin), _ptr(status), _ptr(ws), ws.numel(), st)
+            del ws
+        cap = int(split.caps.get(W, loc_cap))
+        words = _lib.size("dps_tiles_slice_words", NV, tr, cap)
+        sl = self._empty(words, torch.int32)
+        _lib.call("dps_tiles_pack", _ptr(loc_off), _ptr(loc_maxc), _ptr(loc_gmin), _ptr(loc_ent),
+                  NV, tl, tr, cap, _ptr(sl), _ptr(status), st)
+        gathered = self._empty(split.world * words, torch.int32)
+        split.allgather(sl[:words], gathered[: split.world * words])
+        off = self._empty(NV * T + 1, torch.int32)
+        maxc = self._empty(NV * T + 1, torch.int32)
+        gm = self._empty(T, torch.int64) if gmin else None
+        ent = self._empty(ent_cap, torch.int32)
+        ws = self._ws(_lib.size("dps_tiles_assemble_workspace_size", NV, split.world))
+        _lib.call("dps_tiles_assemble", _ptr(gathered), split.world, NV, T, tr, cap, _ptr(off),
+                  _ptr(ent), ent.numel(), _ptr(maxc), _ptr(gm), _ptr(status), _ptr(ws), ws.numel(),
+                  st)
+        # the slice's entry words, for the plan (read by check())
+        self._split_state[W] = loc_off[NV * tl: NV * tl + 1] if tl else None
+        return off, ent, maxc, gm, status
+
+    def _split_plan(self):
+        """After a split build (collective: every rank calls it): the largest
+        slice over the ranks per tile width becomes the gather capacity of the
+        next builds."""
+        split = self.split
+        for W, t in self._split_state.items():
+            words = int(t.item()) if t is not None else 0
+            split.caps[W] = (split.allreduce_max(words) + 3) // 4 * 4
+
     def check(self):
         """Read the build's statistics back (one synchronisation) and raise if a
         value exceeds the engine's integer widths.  Fills ``info``."""
@@ -386,6 +487,12 @@ class PathSimEngine:
         status_h = int(host[L + 3])
         if int(host[L + 4]) != 0:             # impossible by construction (raw >= distinct)
             raise RuntimeError("a row's SpGEMM expansion exceeds its host bound")
+        if status_h == DPS_ERR_OVERFLOW and self.split is not None and self.split.world > 1 \
+                and self.info.max_c <= 0xFFFF:
+            raise RuntimeError("a tile slice outgrew the gather capacity of the split build's plan")
+        if self.split is not None and self.split.world > 1 and self._split_state and \
+                not all(W in self.split.caps for W in self._split_state):
+            self._split_plan()
         if info.expand > self.bounds.sum_c:   # impossible by construction (raw >= distinct)
             raise RuntimeError(f"nnz(C) {info.expand} exceeds its bound {self.bounds.sum_c}")
         if status_h != 0 or info.max_c > 0xFFFF:

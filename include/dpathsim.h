@@ -549,6 +549,50 @@ int dps_unpack_gathered(const int64_t* gathered, int32_t world, int64_t m, int32
                         int64_t* out_cnt, double* out_score, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * A5 operand layout split across ranks (N > 1).  Each rank
+ * builds the C^T tiles of its own target-tile range and the ranks all-gather
+ * the slices; C, s, g and the target order stay replicated.  Replaces the
+ * per-executor re-join of the whole graph the Spark job does for every target
+ * (DPathSim_APVPA.py:72-76 inside the session of :146-168).
+ * dps_label_rows: sub-C of the target labels [l0, l1) in label order --
+ *   sub_ptr int64[l1-l0+1], row i = C row t_perm[l0+i] (t_perm NULL =
+ *   identity) -- so that dps_ct_tiles_build(2) over it with t_rank = NULL,
+ *   g = g_t + l0 and n_targets = l1-l0 builds exactly tiles l0/W .. of the
+ *   full build (l0 a multiple of tile_w).  sub_col / sub_val capacity: the
+ *   rows' total length (e.g. nnz(C)).  ws: dps_label_rows_workspace_size(l1-l0).
+ * dps_tiles_slice_words: uint32 words of one rank's slice for n_mids mids,
+ *   tiles_per_rank tiles and at most ent_cap entry words.
+ * dps_tiles_pack: one rank's build of n_tiles <= tiles_per_rank tiles
+ *   (tile_off / tile_maxc [n_mids*n_tiles+1], tile_gmin [n_tiles], tile_ent;
+ *   maxc / gmin nullable) into its slice; entries beyond ent_cap words set
+ *   *overflow = DPS_ERR_OVERFLOW (nullable) and are not copied.
+ * dps_tiles_assemble: the gathered slices (rank r at r * slice_words, rank r
+ *   owning tiles [r*tiles_per_rank, ...) of n_tiles) -> the full tile_off /
+ *   tile_ent / tile_maxc / tile_gmin of dps_ct_tiles_build, bucket for bucket
+ *   (each bucket's entries in the slice build's order); tile_ent holds
+ *   ent_words words.  A slice whose offsets leave its capacity, a layout
+ *   larger than ent_words, or a nonzero *status on entry (the slice build's
+ *   own status) leaves every bucket empty with *status = DPS_ERR_OVERFLOW (or
+ *   the status it had): the tiles are never read out of bounds.  ws:
+ *   dps_tiles_assemble_workspace_size(n_mids, world).
+ * ------------------------------------------------------------------------- */
+size_t dps_label_rows_workspace_size(int64_t n);
+int dps_label_rows(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                   const int32_t* t_perm, int64_t l0, int64_t l1, int64_t* sub_ptr,
+                   int32_t* sub_col, int32_t* sub_val, void* ws, size_t ws_bytes, void* stream);
+int64_t dps_tiles_slice_words(int64_t n_mids, int64_t tiles_per_rank, int64_t ent_cap);
+int dps_tiles_pack(const uint32_t* tile_off, const uint32_t* tile_maxc, const int64_t* tile_gmin,
+                   const uint32_t* tile_ent, int64_t n_mids, int64_t n_tiles,
+                   int64_t tiles_per_rank, int64_t ent_cap, uint32_t* slice, int32_t* overflow,
+                   void* stream);
+size_t dps_tiles_assemble_workspace_size(int64_t n_mids, int32_t world);
+int dps_tiles_assemble(const uint32_t* gathered, int32_t world, int64_t n_mids, int64_t n_tiles,
+                       int64_t tiles_per_rank, int64_t ent_cap, uint32_t* tile_off,
+                       uint32_t* tile_ent, int64_t ent_words, uint32_t* tile_maxc,
+                       int64_t* tile_gmin, int32_t* status, void* ws, size_t ws_bytes,
+                       void* stream);
+
+/* ---------------------------------------------------------------------------
  * RCCL over xGMI: one rank per process and GPU.  Replaces
  * the Spark shuffle that brings results back to the driver (the .count()
  * actions DPathSim_APVPA.py:86,107 over the session of :146-168).
@@ -567,6 +611,9 @@ int dps_comm_init(void** comm_out, int32_t nranks, int32_t rank, const uint8_t* 
 int dps_comm_destroy(void* comm);
 int dps_bcast(void* comm, void* buf, size_t bytes, int32_t root, void* stream);
 int dps_gather(void* comm, const void* send, void* recv, size_t bytes, int32_t root, void* stream);
+/* dps_allgather: every rank's `bytes` bytes of send into recv on EVERY rank,
+ *   rank r at recv + r * bytes (the tile slices of the N > 1 build). */
+int dps_allgather(void* comm, const void* send, void* recv, size_t bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * A8. Run-log format (DPathSim_APVPA.py:32-67), host-side, for all-pairs

@@ -274,6 +274,94 @@ def _engine_worker(rank, world, port, k, result_path):
         dist.destroy_process_group()
 
 
+def _tilesplit_cpu_worker(rank, world, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dpathsim.dist import TileSplit
+        sp = TileSplit.from_group(device="cpu")
+        send = torch.arange(5, dtype=torch.int32) + 100 * rank
+        recv = torch.empty(5 * world, dtype=torch.int32)
+        sp.allgather(send, recv)
+        want = torch.cat([torch.arange(5, dtype=torch.int32) + 100 * r for r in range(world)])
+        ok = torch.equal(recv, want) and sp.allreduce_max(7 * rank + 1) == 7 * (world - 1) + 1
+        ok = ok and (sp.rank, sp.world) == (rank, world)
+        flags = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+        if rank == 0:
+            with open(result_path, "w") as f:
+                f.write("ok" if int(flags) == 1 else "mismatch")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tilesplit_collectives_gloo(tmp_path, world):
+    """dist.TileSplit's all-gather (rank r's slice at r * size) and the plan's
+    max over ranks, over gloo on CPU."""
+    out = tmp_path / "result.txt"
+    mp.start_processes(_tilesplit_cpu_worker, args=(world, _free_port(), str(out)), nprocs=world,
+                       join=True, start_method="spawn")
+    assert out.read_text() == "ok"
+
+
+def _split_worker(rank, world, port, k, result_path):
+    """One rank of a 2-rank job on ONE GPU with the N > 1 build's tile split
+    (dist.TileSplit over gloo): each rank builds its own target-tile range,
+    the slices are all-gathered and assembled; a second build runs with the
+    plan's capacities; the assembled tiles equal the single-GPU build's and the
+    gathered top-k is the oracle's."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pathsim_oracle as po
+        from dpathsim.dist import TileSplit, pack_counts, shard_edges
+        from dpathsim.engine import PathSimEngine, build_engine
+        from dpathsim.synth import synth_config
+        t = synth_config("config3", scale=0.05).typed()
+        na, nv = t.n_authors, t.n_mids
+        eng = PathSimEngine(t, device="cuda:0")
+        eng.split = TileSplit.from_group(device="cuda:0")
+        eng.upload().build()                     # first build + the plan (collective)
+        caps = dict(eng.split.caps)
+        eng.build()                              # with the plan's capacities
+        ok = eng.split.caps == caps and all(v > 0 for v in caps.values())
+        ref = build_engine(t, device="cuda:0")
+        for w, o_n, m_n in ((16384, "tile_off", "tile_maxc"), (8192, "half_off", "half_maxc")):
+            T = -(-na // w)
+            ok = ok and torch.equal(ref.tensor(o_n)[: nv * T + 1], eng.tensor(o_n)[: nv * T + 1])
+            ok = ok and torch.equal(ref.tensor(m_n)[: nv * T], eng.tensor(m_n)[: nv * T])
+        edges = shard_edges(eng.tensor("row_terms")[:na], world)
+        e = edges.cpu().tolist()
+        bounds = [(e[r], e[r + 1]) for r in range(world)]
+        r0, r1 = bounds[rank]
+        m = max_shard(na, world, bounds)
+        out = tuple(torch.zeros((m, k), dtype=dt, device=eng.device)
+                    for dt in (torch.int32, torch.int64, torch.float64))
+        eng.topk(k, r0, r1, out=tuple(o[: r1 - r0] for o in out))
+        res = gather_topk_compact(pack_counts(out[0], out[1]), eng.tensor("den")[:na], na, world,
+                                  bounds=bounds, edges=edges)
+        flags = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+        if rank == 0:
+            fi, fc, fs = po.COracle.from_typed(t).topk(k, 0, na)
+            gi, gc, gs = (a.cpu().numpy() for a in res)
+            good = (int(flags) == 1 and np.array_equal(gi, fi) and np.array_equal(gc, fc)
+                    and np.array_equal(gs.view(np.int64), fs.view(np.int64)))
+            with open(result_path, "w") as f:
+                f.write("ok" if good else f"mismatch (tiles {int(flags)})")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gloo_two_ranks_split_tile_build(tmp_path):
+    out = tmp_path / "result.txt"
+    mp.start_processes(_split_worker, args=(2, _free_port(), 10, str(out)), nprocs=2,
+                       join=True, start_method="spawn")
+    assert out.read_text() == "ok"
+
+
 @pytest.mark.gpu
 def test_gloo_two_ranks_engine_shards(tmp_path):
     out = tmp_path / "result.txt"
