@@ -104,11 +104,14 @@ def main():
     args.tile_w = eng.tile_w
     if args.venue_skip is not None:
         eng.venue_skip = bool(args.venue_skip) and args.denominator == "rowsum"
-    # N > 1: each rank builds the C^T tiles of its own target-tile range and the
-    # slices are all-gathered (dist.TileSplit); C, g and the
-    # target order stay replicated.  DPATHSIM_BENCH_SPLIT=0: every rank builds
-    # every tile (the round-4 build).
-    if world > 1 and os.environ.get("DPATHSIM_BENCH_SPLIT", "1") == "1":
+    # N > 1: DPATHSIM_BENCH_SPLIT=1 -- each rank builds the C^T tiles of its own
+    # target-tile range and the slices are all-gathered (dist.TileSplit,
+    # DESIGN.md §10); C, g and the target order stay replicated.  Off by
+    # default: on one GPU the per-rank slice build measured 1.70-1.77 ms against
+    # 2.0 ms for the whole build, and the all-gather of the padded slices (63 MB
+    # on config3 at N = 8) costs more than that saves (tools/split_balance.py,
+    # profiles/r05/split_balance.txt)
+    if world > 1 and os.environ.get("DPATHSIM_BENCH_SPLIT", "0") == "1":
         eng.split = TileSplit.from_group(comm=comm, device=dev)
     eng.upload()
 

@@ -418,12 +418,14 @@ __device__ __forceinline__ void sort_venues(const CctParams& p, int d0, int lane
 }
 
 // Venue skipping state of venue lane j in one VGPR: the bits of an fp32 upper
-// bound of C[x,v] / s_v with the low 7 mantissa bits replaced by slot + 1 (0 =
-// not a heavy venue).  Rounding the ratio up to a multiple of 2^-16 relative
-// first keeps the packed value an upper bound.
+// bound of C[x,v] / s_v with the low 7 mantissa bits replaced by slot + 1
+// (kHvNone, a NaN, = not a heavy venue: it compares false with every
+// threshold, so the H ballot is one compare).  Rounding the ratio up to a
+// multiple of 2^-16 relative first keeps the packed value an upper bound.
 constexpr uint32_t kHvSlot = 0x7Fu;
+constexpr uint32_t kHvNone = 0xFFFFFFFFu;
 __device__ __forceinline__ uint32_t hv_pack(float ratio_up, int slot) {
-  if (slot < 0) return 0u;
+  if (slot < 0) return kHvNone;
   const uint32_t b = (__float_as_uint(ratio_up) & ~kHvSlot) + (kHvSlot + 1u);
   return b | static_cast<uint32_t>(slot + 1);
 }
@@ -844,7 +846,6 @@ __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __
 #if DPS_PRIO_ISSUE
   __builtin_amdgcn_s_setprio(DPS_PRIO_ISSUE);
 #endif
-  const bool vl = lane < S.G.nv;
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const int q0 = b * (kWave * kU) + u * kWave;   // wave-uniform
@@ -854,8 +855,8 @@ __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __
     const int q = q0 + lane;
     const bool live = q < S.G.nq;
     const int qlast = min(q0 + kWave - 1, S.G.nq - 1);
-    const int jlo = __popcll(ballot(vl && S.G.pre <= q0)) - 1;
-    const int jhi = __popcll(ballot(vl && S.G.pre <= qlast)) - 1;
+    const int jlo = __popcll(ballot(S.G.pre <= q0)) - 1;
+    const int jhi = __popcll(ballot(S.G.pre <= qlast)) - 1;
     uint32_t bj = readlane(S.G.base, jlo);
     int cj = readlane(S.G.c, jlo);
     if (jhi > jlo) {
@@ -1075,7 +1076,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       };
       // venue skipping: lane j < d0 holds venue j's heavy-table slot (-1: none)
       // and an upper bound of C[x,v] / s_v (s_v >= C[x,v] > 0)
-      uint32_t hv = 0;          // hv_pack(C[x,v] / s_v rounded up, slot)
+      uint32_t hv = kHvNone;    // hv_pack(C[x,v] / s_v rounded up, slot)
       uint64_t hm = 0;          // H: venue lanes no longer scattered
       if (HV && lane < d0) {
         const int sl = kcold(hv_slot)[v];
@@ -1136,7 +1137,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
                 const float gs = X.gsf;
                 const float r = static_cast<float>(tau) * (gxf + gs) * (0.5f * (1.0f - 0x1p-19f)) -
                                 rho * gs * (1.0f + 0x1p-17f);
-                const int m1 = r >= 2147483000.0f ? INT32_MAX : r > 1.0f ? static_cast<int>(ceilf(r)) : 1;
+                // (selects, not branches: r is per lane)
+                const int m1c = static_cast<int>(ceilf(fminf(fmaxf(r, 1.0f), 2147483000.0f)));
+                const int m1 = r >= 2147483000.0f ? INT32_MAX : m1c;
                 const int m2 = mneed_lo32(static_cast<float>(tau), gxf + gs) - X.ubh;
                 mseg = m1 > m2 ? m1 : m2;
               } else {
@@ -1177,10 +1180,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
                   // upper bound of the ratio, th a lower bound of tau / 2); with
                   // every venue in H no target can reach tau
                   const float th = static_cast<float>(tau) * (0.5f * (1.0f - 0x1p-20f));
-                  const uint64_t h2 = ballot(hv != 0u && hv_ratio(hv) <= th);
+                  const uint64_t h2 = ballot(hv_ratio(hv) <= th);   // (kHvNone: false)
                   hchg = h2 != hm;
                   hm = h2;
-                  row_done = d <= kWave && hm == ballot(lane < d0);
+                  row_done = d <= kWave && __popcll(hm) == d0;   // hm is within lanes < d0
                 }
               }
               // (an overflowed opt tile's halves are queued behind the

@@ -158,11 +158,11 @@ __device__ __forceinline__ float i64_f32(int64_t v) {   // v >= 0
   return __uint2float_rn(static_cast<uint32_t>(u >> 32)) * 4294967296.0f +
          __uint2float_rn(static_cast<uint32_t>(u));
 }
+// (selects, not branches: den is per lane in the segment thresholds)
 __device__ __forceinline__ int mneed_lo32(float kth, float den) {
-  if (!(kth > 0.0f) || !(den > 0.0f)) return 0;
   const float r = kth * den * (0.5f * (1.0f - 0x1p-19f));
-  if (r >= 2147483000.0f) return INT32_MAX;
-  return static_cast<int>(ceilf(r));
+  const int m = static_cast<int>(ceilf(fminf(fmaxf(r, 0.0f), 2147483000.0f)));
+  return !(kth > 0.0f) || !(den > 0.0f) ? 0 : r >= 2147483000.0f ? INT32_MAX : m;
 }
 
 // Register-resident sorted top-k of one wave: rank r*64 + lane in slot r.
