@@ -731,12 +731,27 @@ __device__ __forceinline__ void acc_add4(uint32_t* acc, uint32_t h, int c, int l
   __hip_atomic_fetch_add(acc + (local >> tpds), add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// A batch into the accumulator: the base pass by the shared branch-free u8 /
-// 4-bit path, wide passes entry by entry (u8h: u8-format entries).
+// A batch into the accumulator: the base pass branch-free over the loads
+// batch b issued (the u8 / 4-bit adds: dead lanes add 0, see kDeadChunk),
+// wide passes entry by entry (u8h: u8-format entries).
 template <int F>
-__device__ __forceinline__ void scatter_f(const Batch& B, const Stage& S, uint32_t* acc, bool u8h) {
-  if (F == 1 || u8h || S.lnp == 0) {
-    scatter_any<true>(B, S, acc, 0u, kLabMask1, Fmt<1>::S);
+__device__ __forceinline__ void scatter_f(const Batch& B, const Stage& S, int b, uint32_t* acc,
+                                          bool u8h) {
+  if (S.lnp == 0) {                                    // u8 or 4-bit base pass
+    const int left = S.G.nq - b * (kWave * kU);        // chunks from this batch on (uniform)
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (u * kWave >= left) break;                    // a load issue1 skipped
+      const uint32_t c = static_cast<uint32_t>(B.c[u]);
+      add_u8_word<true>(0u, B.e[u].x, c, kLabMask1);
+      add_u8_word<true>(0u, B.e[u].y, c, kLabMask1);
+      add_u8_word<true>(0u, B.e[u].z, c, kLabMask1);
+      add_u8_word<true>(0u, B.e[u].w, c, kLabMask1);
+    }
+    return;
+  }
+  if (F == 1 || u8h) {                                 // u8-format wide passes
+    scatter<true>(B, S, acc, Fmt<1>::S);
     return;
   }
 #pragma unroll
@@ -830,6 +845,44 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
 #ifndef DPS_KSEL
 #define DPS_KSEL 2
 #endif
+// The chunk a dead lane (past the stage's last chunk) loads instead of a real
+// one: lane L's 16-bit entries all address accumulator dword L (h = L << 5 in
+// both the u8 and the 4-bit format), and the lane's C is 0, so its adds are
+// no-ops on 64 distinct dwords -- no per-lane branch around the adds, and no
+// 64-way conflict on one dword (which the branch used to avoid).
+__device__ uint4 kDeadChunk[kWave] = {   // (global, not constant: one global_load)
+    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u}, {0x00200020u, 0x00200020u, 0x00200020u, 0x00200020u},
+    {0x00400040u, 0x00400040u, 0x00400040u, 0x00400040u}, {0x00600060u, 0x00600060u, 0x00600060u, 0x00600060u},
+    {0x00800080u, 0x00800080u, 0x00800080u, 0x00800080u}, {0x00A000A0u, 0x00A000A0u, 0x00A000A0u, 0x00A000A0u},
+    {0x00C000C0u, 0x00C000C0u, 0x00C000C0u, 0x00C000C0u}, {0x00E000E0u, 0x00E000E0u, 0x00E000E0u, 0x00E000E0u},
+    {0x01000100u, 0x01000100u, 0x01000100u, 0x01000100u}, {0x01200120u, 0x01200120u, 0x01200120u, 0x01200120u},
+    {0x01400140u, 0x01400140u, 0x01400140u, 0x01400140u}, {0x01600160u, 0x01600160u, 0x01600160u, 0x01600160u},
+    {0x01800180u, 0x01800180u, 0x01800180u, 0x01800180u}, {0x01A001A0u, 0x01A001A0u, 0x01A001A0u, 0x01A001A0u},
+    {0x01C001C0u, 0x01C001C0u, 0x01C001C0u, 0x01C001C0u}, {0x01E001E0u, 0x01E001E0u, 0x01E001E0u, 0x01E001E0u},
+    {0x02000200u, 0x02000200u, 0x02000200u, 0x02000200u}, {0x02200220u, 0x02200220u, 0x02200220u, 0x02200220u},
+    {0x02400240u, 0x02400240u, 0x02400240u, 0x02400240u}, {0x02600260u, 0x02600260u, 0x02600260u, 0x02600260u},
+    {0x02800280u, 0x02800280u, 0x02800280u, 0x02800280u}, {0x02A002A0u, 0x02A002A0u, 0x02A002A0u, 0x02A002A0u},
+    {0x02C002C0u, 0x02C002C0u, 0x02C002C0u, 0x02C002C0u}, {0x02E002E0u, 0x02E002E0u, 0x02E002E0u, 0x02E002E0u},
+    {0x03000300u, 0x03000300u, 0x03000300u, 0x03000300u}, {0x03200320u, 0x03200320u, 0x03200320u, 0x03200320u},
+    {0x03400340u, 0x03400340u, 0x03400340u, 0x03400340u}, {0x03600360u, 0x03600360u, 0x03600360u, 0x03600360u},
+    {0x03800380u, 0x03800380u, 0x03800380u, 0x03800380u}, {0x03A003A0u, 0x03A003A0u, 0x03A003A0u, 0x03A003A0u},
+    {0x03C003C0u, 0x03C003C0u, 0x03C003C0u, 0x03C003C0u}, {0x03E003E0u, 0x03E003E0u, 0x03E003E0u, 0x03E003E0u},
+    {0x04000400u, 0x04000400u, 0x04000400u, 0x04000400u}, {0x04200420u, 0x04200420u, 0x04200420u, 0x04200420u},
+    {0x04400440u, 0x04400440u, 0x04400440u, 0x04400440u}, {0x04600460u, 0x04600460u, 0x04600460u, 0x04600460u},
+    {0x04800480u, 0x04800480u, 0x04800480u, 0x04800480u}, {0x04A004A0u, 0x04A004A0u, 0x04A004A0u, 0x04A004A0u},
+    {0x04C004C0u, 0x04C004C0u, 0x04C004C0u, 0x04C004C0u}, {0x04E004E0u, 0x04E004E0u, 0x04E004E0u, 0x04E004E0u},
+    {0x05000500u, 0x05000500u, 0x05000500u, 0x05000500u}, {0x05200520u, 0x05200520u, 0x05200520u, 0x05200520u},
+    {0x05400540u, 0x05400540u, 0x05400540u, 0x05400540u}, {0x05600560u, 0x05600560u, 0x05600560u, 0x05600560u},
+    {0x05800580u, 0x05800580u, 0x05800580u, 0x05800580u}, {0x05A005A0u, 0x05A005A0u, 0x05A005A0u, 0x05A005A0u},
+    {0x05C005C0u, 0x05C005C0u, 0x05C005C0u, 0x05C005C0u}, {0x05E005E0u, 0x05E005E0u, 0x05E005E0u, 0x05E005E0u},
+    {0x06000600u, 0x06000600u, 0x06000600u, 0x06000600u}, {0x06200620u, 0x06200620u, 0x06200620u, 0x06200620u},
+    {0x06400640u, 0x06400640u, 0x06400640u, 0x06400640u}, {0x06600660u, 0x06600660u, 0x06600660u, 0x06600660u},
+    {0x06800680u, 0x06800680u, 0x06800680u, 0x06800680u}, {0x06A006A0u, 0x06A006A0u, 0x06A006A0u, 0x06A006A0u},
+    {0x06C006C0u, 0x06C006C0u, 0x06C006C0u, 0x06C006C0u}, {0x06E006E0u, 0x06E006E0u, 0x06E006E0u, 0x06E006E0u},
+    {0x07000700u, 0x07000700u, 0x07000700u, 0x07000700u}, {0x07200720u, 0x07200720u, 0x07200720u, 0x07200720u},
+    {0x07400740u, 0x07400740u, 0x07400740u, 0x07400740u}, {0x07600760u, 0x07600760u, 0x07600760u, 0x07600760u},
+    {0x07800780u, 0x07800780u, 0x07800780u, 0x07800780u}, {0x07A007A0u, 0x07A007A0u, 0x07A007A0u, 0x07A007A0u},
+    {0x07C007C0u, 0x07C007C0u, 0x07C007C0u, 0x07C007C0u}, {0x07E007E0u, 0x07E007E0u, 0x07E007E0u, 0x07E007E0u}};
 constexpr int kSel = DPS_KSEL;
 
 // The wave raises its issue priority while it computes and issues a batch of
@@ -875,7 +928,11 @@ __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __
         cj = __shfl(S.G.c, j, kWave);
       }
     }
-    B.e[u] = *reinterpret_cast<const uint4*>(ent + (live ? bj + 4u * static_cast<uint32_t>(q) : 0u));
+    // (the offset wraps in 32 bits on purpose: base_j = lo_j - 4 pre_j may be
+    // "negative", base_j + 4q is not)
+    const uint32_t off = bj + 4u * static_cast<uint32_t>(q);
+    const uint4* src = live ? reinterpret_cast<const uint4*>(ent + off) : kDeadChunk + lane;
+    B.e[u] = *src;
     B.c[u] = live ? cj : 0;
   }
 #if DPS_PRIO_ISSUE
@@ -909,7 +966,7 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
     for (int b = 0; b < E.nb; ++b) {
       Batch B;
       issue1(E, b, ent, lane, B);
-      scatter_f<F>(B, E, acc, u8h);
+      scatter_f<F>(B, E, b, acc, u8h);
     }
   }
   return chunks;
@@ -1107,11 +1164,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
             if (prof) ts[0] = __builtin_amdgcn_s_memtime();
             const uint32_t* ent = X.u8h ? p.h_ent : p.tile_ent;
             if (X.S.pass > 0) issue1(X.S, 0, ent, lane, B);
-            scatter_f<F>(B, X.S, acc, X.u8h);
+            scatter_f<F>(B, X.S, 0, acc, X.u8h);
             for (int b = 1; b < X.S.nb; ++b) {
               Batch B2;
               issue1(X.S, b, ent, lane, B2);
-              scatter_f<F>(B2, X.S, acc, X.u8h);
+              scatter_f<F>(B2, X.S, b, acc, X.u8h);
             }
             n_chunk += static_cast<uint64_t>(X.S.G.nq);
             ++n_pass;

@@ -1,4 +1,6 @@
-"""Drive tools/mfma_probe/probe.hip on config3's heavy-venue panel (research).
+"""Drive tools/mfma_probe/probe.hip on a config's heavy-venue panel (research;
+PROBE_CONFIG, default config3; config5 for the round-5 A/B at BASELINE
+config 5's shape, PROBE_K the list of panel widths).
 
 Builds the engine, takes the K venues with the most authors (largest n_v, so
 largest n_v^2), lays C[y, v] (v heavy, clamped to 127) out as a dense i8 panel
@@ -23,7 +25,10 @@ from dpathsim.synth import synth_config
 lib = ctypes.CDLL(os.path.join(HERE, "libmfmaprobe.so"))
 lib.probe_run.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
                           ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-t = synth_config("config3").typed()
+from dpathsim.synth import CONFIGS
+cfg = os.environ.get("PROBE_CONFIG", "config3")
+kk = CONFIGS[cfg][4]
+t = synth_config(cfg).typed()
 eng = build_engine(t)
 NA, NV = t.n_authors, t.n_mids
 nnz = eng.info.nnz_c
@@ -34,12 +39,21 @@ val = eng.tensor("c_val")[:nnz]
 rank = eng.tensor("t_rank")[:NA].long()
 row = torch.repeat_interleave(torch.arange(NA, device=dev), c_ptr[1:] - c_ptr[:-1])
 n_v = torch.bincount(col, minlength=NV)
-idx, cnt, sc = eng.topk(10)
+idx, cnt, sc = eng.topk(kk)
+torch.cuda.synchronize()
+# the SIMT hot kernel itself, timed in the same process (and rocprof profile)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+eng.topk(kk)
+e1.record()
+torch.cuda.synchronize()
+print(json.dumps({"config": cfg, "k": kk, "simt_topk_ms": e0.elapsed_time(e1),
+                  "n_authors": NA, "n_mids": NV}), flush=True)
 kth_m = cnt[:, -1].to(torch.int32)          # the k-th entry's count per row (original order)
 thr_real = torch.empty(NA, dtype=torch.int32, device=dev)
 thr_real[rank] = torch.clamp(kth_m, min=1)
 res = []
-for K in (32, 64, 128):
+for K in [int(v) for v in os.environ.get("PROBE_K", "32,64,128").split(",")]:
     heavy = torch.argsort(n_v, descending=True)[:K]
     hmap = torch.full((NV,), -1, dtype=torch.long, device=dev)
     hmap[heavy] = torch.arange(K, device=dev)
@@ -59,7 +73,8 @@ for K in (32, 64, 128):
     want = torch.zeros_like(dump)
     want[0:32], want[64:96] = full[0:32], full[64:96]
     ok = bool(torch.equal(dump, want))
-    out = {"K": K, "heavy_share_of_terms": share, "verify_block_exact": ok, "rc": rc}
+    out = {"config": cfg, "K": K, "heavy_share_of_terms": share, "verify_block_exact": ok,
+           "rc": rc}
     for name, thr in (("no_candidates", thr_none), ("kth_count_threshold", thr_real)):
         counter.zero_()
         lib.probe_run(panel.data_ptr(), NA, K, thr.data_ptr(), NA, counter.data_ptr(), None, st)
