@@ -514,6 +514,42 @@ template <int KPL, bool HV, bool SY>
 __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& top, int n,
                                          int64_t gx, int lane, int c, uint32_t hv, uint64_t hm,
                                          RowAux& ra) {
+  if constexpr (!SY) {
+    // branch-free: every lane scores (lanes past n read target 0, in bounds,
+    // and are masked out), so no exec-mask branches around the loads and the
+    // division; the better-than-k-th test is three ballots of one compare each
+    const int lab = lane < n ? Q.lab0 : 0;
+    int M = Q.m0;
+    ra.cand += static_cast<uint32_t>(n);
+    if (HV && hm) {
+      ra.ver += static_cast<uint32_t>(n);
+      const uint16_t* row = p.hv_c + static_cast<int64_t>(lab) * p.n_hv;
+      for (uint64_t m = hm; m; m &= m - 1) {          // wave-uniform, |H| is small
+        const int j = __builtin_ctzll(m);
+        const int a = readlane(c, j);
+        const int sl = static_cast<int>(readlane(hv, j) & kHvSlot) - 1;
+        M += a * static_cast<int>(row[sl]);
+      }
+    }
+    const int yo = p.t_perm ? p.t_perm[lab] : lab;
+    const int64_t den = gx + p.g_t[lab];
+    const double sc = static_cast<double>(2 * static_cast<int64_t>(M)) / static_cast<double>(den);
+    const uint64_t live = n >= kWave ? ~0ull : ((1ull << n) - 1ull);
+    uint64_t mask = live & (ballot(sc > top.kth_s) |
+                            (ballot(sc == top.kth_s) & ballot(yo < top.kth_y)));
+    if (n >= kWave) { Q.lab0 = Q.lab1; Q.m0 = Q.m1; }
+    Q.n -= n;
+    while (mask) {
+      const int srcl = __ffsll(static_cast<long long>(mask)) - 1;
+      mask &= mask - 1;
+      const double cs = readlane(sc, srcl);
+      const int cy = readlane(yo, srcl);
+      if (!better(cs, cy, top.kth_s, top.kth_y)) continue;
+      ++ra.ins;
+      top.insert(cs, cy, readlane(M, srcl));
+    }
+    return;
+  }
   bool cand = lane < n;
   int M = 0, yo = 0;
   double sc = 0.0;
@@ -647,7 +683,7 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
     }
 
     const int i0 = (blk << kSeg) + (lane << 5);
-    if (xin) {                                     // the source itself never counts
+    if (__builtin_expect(xin, false)) {            // the source itself never counts
       const int rel = xrel - i0;
       if (rel >= 0 && rel < 32) F4 &= ~(1u << ((rel & 7) * 4 + 3 - (rel >> 3)));
     }
@@ -656,17 +692,16 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
       const bool has = F4 != 0;
       const uint64_t mk = ballot(has);
       if (!mk) break;
-      int lab = 0, mv = 0;
-      if (has) {
-        const int bit = __builtin_ctz(F4);
-        F4 &= F4 - 1;
-        const int nib = bit >> 2, dw = 3 - (bit & 3);
-        const uint32_t w01 = (dw & 1) ? a.y : a.x;
-        const uint32_t w23 = (dw & 1) ? a.w : a.z;
-        const uint32_t wv = (dw & 2) ? w23 : w01;
-        lab = static_cast<int>(tile_base + i0 + dw * 8 + nib);
-        mv = static_cast<int>((wv >> (nib * 4)) & 0xFu);
-      }
+      // every lane extracts (a lane without a flag gets garbage that vq_push
+      // never stores): no exec-mask branch per round
+      const int bit = __builtin_ffs(static_cast<int>(F4)) - 1;    // -1 when F4 == 0
+      F4 &= F4 - 1;
+      const int nib = (bit >> 2) & 7, dw = 3 - (bit & 3);
+      const uint32_t w01 = (dw & 1) ? a.y : a.x;
+      const uint32_t w23 = (dw & 1) ? a.w : a.z;
+      const uint32_t wv = (dw & 2) ? w23 : w01;
+      const int lab = static_cast<int>(tile_base + i0 + dw * 8 + nib);
+      const int mv = static_cast<int>((wv >> (nib * 4)) & 0xFu);
       vq_push(Q, has, lab, mv, mk, lane);
       if (Q.n >= kWave) {
         if (hold) {         // an unverified half may not be flushed: give it up
@@ -796,7 +831,7 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
     }
     // target (4*dw + byte) of this lane's 16 -> bit 8*byte + 7 - dw
     const int i0 = (blk << kSeg1) + (lane << 4);
-    if (xin) {                                    // the source itself never counts
+    if (__builtin_expect(xin, false)) {           // the source itself never counts
       const int rel = xrel - i0;
       if (rel >= 0 && rel < 16) F &= ~(1u << ((rel & 3) * 8 + 7 - (rel >> 2)));
     }
@@ -805,17 +840,15 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
       const bool has = F != 0;
       const uint64_t mk = ballot(has);
       if (!mk) break;
-      int lab = 0, mv = 0;
-      if (has) {
-        const int bit = __builtin_ctz(F);
-        F &= F - 1;
-        const int byte = bit >> 3, dw = 7 - (bit & 7);
-        const uint32_t w01 = (dw & 1) ? a.y : a.x;
-        const uint32_t w23 = (dw & 1) ? a.w : a.z;
-        const uint32_t wv = (dw & 2) ? w23 : w01;
-        lab = static_cast<int>(tile_base + i0 + dw * 4 + byte);
-        mv = static_cast<int>((wv >> (byte * 8)) & 0xFFu);
-      }
+      // every lane extracts (as in epi1_u4: no exec-mask branch per round)
+      const int bit = __builtin_ffs(static_cast<int>(F)) - 1;    // -1 when F == 0
+      F &= F - 1;
+      const int byte = (bit >> 3) & 3, dw = 7 - (bit & 7);
+      const uint32_t w01 = (dw & 1) ? a.y : a.x;
+      const uint32_t w23 = (dw & 1) ? a.w : a.z;
+      const uint32_t wv = (dw & 2) ? w23 : w01;
+      const int lab = static_cast<int>(tile_base + i0 + dw * 4 + byte);
+      const int mv = static_cast<int>((wv >> (byte * 8)) & 0xFFu);
       vq_push(Q, has, lab, mv, mk, lane);
       if (Q.n >= kWave) vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
     }

@@ -201,8 +201,12 @@ struct TopK {
     int pos = 0;
 #pragma unroll
     for (int r = 0; r < KPL; ++r) {
-      const bool b = (r * kWave + lane < k) && better(s[r], y[r], cs, cy);
-      pos += __popcll(ballot(b));
+      // slots r*64 + lane < k that rank above the candidate: ballots of one
+      // compare each (a ballot of a compound predicate materialises it)
+      const int nv = k - r * kWave;
+      const uint64_t valid = nv >= kWave ? ~0ull : nv <= 0 ? 0ull : ((1ull << nv) - 1ull);
+      const uint64_t b = ballot(s[r] > cs) | (ballot(s[r] == cs) & ballot(y[r] < cy));
+      pos += __popcll(b & valid);
     }
     double us[KPL];
     int uy[KPL], um[KPL];
@@ -223,10 +227,12 @@ struct TopK {
       }
     }
 #pragma unroll
-    for (int r = 0; r < KPL; ++r) {
+    for (int r = 0; r < KPL; ++r) {     // selects, not branches
       const int slot = r * kWave + lane;
-      if (slot > pos) { s[r] = us[r]; y[r] = uy[r]; m[r] = um[r]; }
-      else if (slot == pos) { s[r] = cs; y[r] = cy; m[r] = cm; }
+      const bool up = slot > pos, at = slot == pos;
+      s[r] = up ? us[r] : at ? cs : s[r];
+      y[r] = up ? uy[r] : at ? cy : y[r];
+      m[r] = up ? um[r] : at ? cm : m[r];
     }
     filled = filled < k ? filled + 1 : k;
     if (floored && filled < k) return;   // the floor stays the threshold

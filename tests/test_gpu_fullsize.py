@@ -7,9 +7,9 @@ the 256 heaviest split into target-tile pieces, dps_topk_merge):
   format (tile_w 8192) identical to it on every row;
 * config4 (APTPA, 200k topics, top-10): EVERY row;
 * config5 (3M authors, 20k venues, top-100, two top-k registers per lane):
-  every third row plus the 2000 heaviest rows plus every row whose per-tile
-  bound sum_v C[x,v] * maxc[v,t] exceeds 255 in some tile (the rows that can
-  take the wide accumulator passes);
+  EVERY row, in three tests of a million rows each (the rows whose per-tile
+  bound sum_v C[x,v] * maxc[v,t] exceeds 255 in some tile -- the rows that can
+  take the wide accumulator passes -- are checked to be present);
 * a crafted graph whose counts force the wide passes at tile_w 8192 and 16384;
 * config 2 stand-in (dblp_large.gexf is absent, .MISSING_LARGE_BLOBS:1;
   SURVEY §8d): config3_100k written as GEXF, re-read by the streaming loader
@@ -116,23 +116,34 @@ def _wide_bound_rows(eng, t, cap=3000):
     return np.asarray(out, dtype=np.int64)
 
 
-def test_config5_strided_heaviest_and_wide_bound_rows():
+@pytest.fixture(scope="module")
+def config5_run():
+    """Config5 (3M authors, 20k venues, top-100) through the bench path once:
+    the engine's all-rows top-k on the host, the C oracle, the wide-bound rows."""
     import pathsim_oracle as po
     from dpathsim.engine import build_engine
     from dpathsim.synth import synth_config
     t = synth_config("config5").typed()
     eng = build_engine(t)
-    work = eng.row_work().cpu().numpy()
     wide = _wide_bound_rows(eng, t)
+    got = [a.cpu().numpy() for a in eng.topk(100)]   # bench path, k = 100
+    del eng
+    return t, got, wide, po.COracle.from_typed(t)
+
+
+@pytest.mark.parametrize("part", [0, 1, 2])
+def test_config5_all_rows(config5_run, part):
+    """Every config5 row, bit-exact, in three parts (rows = part mod 3) so each
+    test's oracle run stays within a few minutes; the rows whose per-tile bound
+    exceeds 255 (the wide-pass rows) are among them."""
+    t, got, wide, co = config5_run
     assert len(wide) > 0
-    rows = np.union1d(np.union1d(np.argsort(-work, kind="stable")[:2000], wide),
-                      np.arange(0, t.n_authors, 3))
-    got = [a.cpu().numpy()[rows] for a in eng.topk(100)]   # bench path, k = 100
+    rows = np.arange(part, t.n_authors, 3)
     t0 = time.perf_counter()
-    want = _oracle_rows(po.COracle.from_typed(t), 100, rows, chunk=50_000)
-    print(f"config5: {len(rows)} rows ({len(wide)} with a tile bound > 255), oracle "
-          f"{time.perf_counter() - t0:.1f} s")
-    _cmp(got, want, rows)
+    want = _oracle_rows(co, 100, rows, chunk=100_000)
+    print(f"config5 part {part}: {len(rows)} rows ({np.isin(wide, rows).sum()} with a tile "
+          f"bound > 255), oracle {time.perf_counter() - t0:.1f} s")
+    _cmp([a[rows] for a in got], want, rows)
 
 
 def _crafted_wide_counts(n_fill=20000, seed=5):
