@@ -439,6 +439,10 @@ struct RowAux {
   uint32_t ver = 0, cand = 0, ins = 0;
   uint32_t redo = 0;            // optimistic 4-bit passes that overflowed (counter[4])
   uint32_t u8h = 0, wide = 0;   // profiling build: half-tile and wide passes
+  // profiling build: epilogue blocks by outcome (counter[19..23]): threshold
+  // above the counter width, prefilter empty, exact test empty, with
+  // candidates; and candidate extraction rounds
+  uint32_t bk[5] = {0, 0, 0, 0, 0};
   int x = 0;               // source row (ordinal)
   int far = INT_MAX;       // sym = 2: targets in tiles >= far may go to records
 };
@@ -648,14 +652,14 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
 // 32l..32l+31), read and zeroed kEpi1 at a time; candidates queued as in epi1_u8.
 template <int KPL, bool HV, bool SY>
 __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
-                                        int t, int lane, int64_t x_lab, int64_t gx, int mseg,
+                                        int t, int lane, int x_lab, int64_t gx, int mseg,
                                         int c, uint32_t hv, uint64_t hm, RowAux& ra,
                                         uint32_t bmask, uint32_t oexp, uint32_t& bad) {
   constexpr int kS = Fmt<2>::S, kSeg = Fmt<2>::SEG;
-  const int64_t tile_base = static_cast<int64_t>(t) << kS;
-  const int64_t xr = x_lab - tile_base;
-  const bool xin = xr >= 0 && xr < (int64_t(1) << kS);   // the source is a target of this tile
-  const int xrel = xin ? static_cast<int>(xr) : 0;
+  const int tile_base = t << kS;                         // labels < 2^31
+  const int xr = x_lab - tile_base;
+  const bool xin = static_cast<uint32_t>(xr) < (1u << kS);   // the source is a target of this tile
+  const int xrel = xin ? xr : 0;
   // optimistic pass judged here (oexp != 0, DPS_OPT_INEPI): each half's
   // candidates are held in the queue (no flush) until its digit sum shows no
   // overflowed count; a bad half's candidates are dropped (Q.n back to snap)
@@ -664,9 +668,15 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
   int snap = Q.n;
   auto block = [&](uint4 a, int blk) {
     const uint32_t m = static_cast<uint32_t>(readlane(mseg, blk));
-    if (m > 15u || !((bmask >> blk) & 1u)) return;   // no 4-bit count reaches m / overflowed half
+    if (m > 15u || !((bmask >> blk) & 1u)) {   // no 4-bit count reaches m / overflowed half
+      if (kProfile) ++ra.bk[0];
+      return;
+    }
     const uint32_t pm = (0x10u - (0x80000000u >> __builtin_clz(m))) * 0x11111111u;
-    if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) return;
+    if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) {
+      if (kProfile) ++ra.bk[1];
+      return;
+    }
     // target (8*dw + nib) of this lane's 32 -> bit 4*nib + 3 - dw
     // per-nibble flags (bit 3): nibble >= m, 1 <= m <= 15 (no carry leaves a
     // nibble: low3 + 16 - m <= 14); m is wave-uniform, so one branch per block
@@ -687,11 +697,16 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
       const int rel = xrel - i0;
       if (rel >= 0 && rel < 32) F4 &= ~(1u << ((rel & 7) * 4 + 3 - (rel >> 3)));
     }
-    if (!ballot(F4 != 0)) return;
+    if (!ballot(F4 != 0)) {
+      if (kProfile) ++ra.bk[2];
+      return;
+    }
+    if (kProfile) ++ra.bk[3];
     for (;;) {
       const bool has = F4 != 0;
       const uint64_t mk = ballot(has);
       if (!mk) break;
+      if (kProfile) ++ra.bk[4];
       // every lane extracts (a lane without a flag gets garbage that vq_push
       // never stores): no exec-mask branch per round
       const int bit = __builtin_ffs(static_cast<int>(F4)) - 1;    // -1 when F4 == 0
@@ -700,7 +715,7 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
       const uint32_t w01 = (dw & 1) ? a.y : a.x;
       const uint32_t w23 = (dw & 1) ? a.w : a.z;
       const uint32_t wv = (dw & 2) ? w23 : w01;
-      const int lab = static_cast<int>(tile_base + i0 + dw * 8 + nib);
+      const int lab = tile_base + i0 + dw * 8 + nib;
       const int mv = static_cast<int>((wv >> (nib * 4)) & 0xFu);
       vq_push(Q, has, lab, mv, mk, lane);
       if (Q.n >= kWave) {
@@ -806,19 +821,25 @@ __device__ __forceinline__ void scatter_f(const Batch& B, const Stage& S, int b,
 // at a time; candidates are queued and scored 64 at a time by flush().
 template <int KPL, bool HV, bool SY>
 __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
-                                        int t, int lane, int64_t x_lab, int64_t gx, int mseg,
+                                        int t, int lane, int x_lab, int64_t gx, int mseg,
                                         int c, uint32_t hv, uint64_t hm, RowAux& ra) {
   constexpr int kS1 = Fmt<1>::S, kSeg1 = Fmt<1>::SEG;
-  constexpr int kW1 = 1 << kS1;
-  const int64_t tile_base = static_cast<int64_t>(t) << kS1;
-  const int64_t xr = x_lab - tile_base;
-  const bool xin = xr >= 0 && xr < kW1;          // the source is a target of this tile
-  const int xrel = xin ? static_cast<int>(xr) : 0;
+  constexpr uint32_t kW1 = 1u << kS1;
+  const int tile_base = t << kS1;                        // labels < 2^31
+  const int xr = x_lab - tile_base;
+  const bool xin = static_cast<uint32_t>(xr) < kW1;     // the source is a target of this tile
+  const int xrel = xin ? xr : 0;
   auto block = [&](uint4 a, int blk) {
     const uint32_t m = static_cast<uint32_t>(readlane(mseg, blk));
-    if (m > 255u) return;                         // no u8 count reaches m
+    if (m > 255u) {                               // no u8 count reaches m
+      if (kProfile) ++ra.bk[0];
+      return;
+    }
     const uint32_t pm = (0x100u - (0x80000000u >> __builtin_clz(m))) * 0x01010101u;
-    if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) return;
+    if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) {
+      if (kProfile) ++ra.bk[1];
+      return;
+    }
     uint32_t F;
     if (m <= 128u) {
       const uint32_t kA = (128u - m) * 0x01010101u;
@@ -835,11 +856,16 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
       const int rel = xrel - i0;
       if (rel >= 0 && rel < 16) F &= ~(1u << ((rel & 3) * 8 + 7 - (rel >> 2)));
     }
-    if (!ballot(F != 0)) return;
+    if (!ballot(F != 0)) {
+      if (kProfile) ++ra.bk[2];
+      return;
+    }
+    if (kProfile) ++ra.bk[3];
     for (;;) {
       const bool has = F != 0;
       const uint64_t mk = ballot(has);
       if (!mk) break;
+      if (kProfile) ++ra.bk[4];
       // every lane extracts (as in epi1_u4: no exec-mask branch per round)
       const int bit = __builtin_ffs(static_cast<int>(F)) - 1;    // -1 when F == 0
       F &= F - 1;
@@ -847,7 +873,7 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
       const uint32_t w01 = (dw & 1) ? a.y : a.x;
       const uint32_t w23 = (dw & 1) ? a.w : a.z;
       const uint32_t wv = (dw & 2) ? w23 : w01;
-      const int lab = static_cast<int>(tile_base + i0 + dw * 4 + byte);
+      const int lab = tile_base + i0 + dw * 4 + byte;
       const int mv = static_cast<int>((wv >> (byte * 8)) & 0xFFu);
       vq_push(Q, has, lab, mv, mk, lane);
       if (Q.n >= kWave) vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
@@ -1045,7 +1071,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
   // work counts of this wave (wave-uniform), summed into counter[1..2] at exit:
   // accumulator passes (each reads and zeroes the 8 KiB accumulator) and 16-byte
   // chunks scattered -- the bench's algorithmic LDS bytes
-  uint64_t n_pass = 0, n_chunk = 0;
+  uint32_t n_pass = 0, n_chunk = 0;   // < 2^32 per wave (widened at the exit)
   RowAux ra;       // work counts; the symmetric mode's row state
 
   for (;;) {
@@ -1203,10 +1229,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
               issue1(X.S, b, ent, lane, B2);
               scatter_f<F>(B2, X.S, b, acc, X.u8h);
             }
-            n_chunk += static_cast<uint64_t>(X.S.G.nq);
+            n_chunk += static_cast<uint32_t>(X.S.G.nq);
             ++n_pass;
             if (d > kWave)
-              n_chunk += static_cast<uint64_t>(extra_groups<F>(p, X.S, acc, pb, d, lane, X.u8h));
+              n_chunk += static_cast<uint32_t>(extra_groups<F>(p, X.S, acc, pb, d, lane, X.u8h));
             if (prof) ts[1] = __builtin_amdgcn_s_memtime();
             // score what is queued while the list is filling or the queue is
             // half full (one memory round trip per 64 candidates)
@@ -1427,6 +1453,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
     atomicAdd(p.counter + 16, static_cast<unsigned long long>(ra.ins));
     atomicAdd(p.counter + 17, static_cast<unsigned long long>(ra.u8h));
     atomicAdd(p.counter + 18, static_cast<unsigned long long>(ra.wide));
+#pragma unroll
+    for (int i = 0; i < 5; ++i) atomicAdd(p.counter + 19 + i, static_cast<unsigned long long>(ra.bk[i]));
   }
 }
 

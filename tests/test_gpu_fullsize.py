@@ -39,6 +39,20 @@ def _cmp(got, want, rows=None):
                              f"orc {oi[bad[0]]} {oc[bad[0]]} {os_[bad[0]]}")
 
 
+def _progress(msg):
+    """Print, and append to gpurun_out/pytest_progress.log: under pytest's
+    output capture (-q without -s) only the file shows that a long oracle run
+    is alive to a watchdog that kills silent commands."""
+    print(msg, flush=True)
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "pytest_progress.log"), "a") as f:
+            f.write(msg + "\n")
+    except OSError:
+        pass
+
+
 def _oracle_rows(co, k, rows, chunk=256):
     """C oracle top-k of a row list in chunks, printing progress (long oracle
     runs must keep writing: the GPU box kills silent commands)."""
@@ -47,8 +61,8 @@ def _oracle_rows(co, k, rows, chunk=256):
     t0 = time.perf_counter()
     for i in range(0, len(rows), chunk):
         parts.append(co.topk_rows(k, rows[i:i + chunk]))
-        print(f"  oracle rows {min(i + chunk, len(rows))}/{len(rows)} "
-              f"({time.perf_counter() - t0:.0f} s)", flush=True)
+        _progress(f"  oracle rows {min(i + chunk, len(rows))}/{len(rows)} "
+                  f"({time.perf_counter() - t0:.0f} s)")
     return tuple(np.concatenate([p[j] for p in parts]) for j in range(3))
 
 

@@ -26,3 +26,7 @@ print(f"passes over u8 half tiles {c[17]} ({c[17] / st:.3f} of stages), with wid
       f"{c[18]} ({c[18] / st:.4f})", flush=True)
 print(f"stages {st} ({st / R:.1f} per row); cycles per wave-stage: " +
       " ".join(f"{n} {c[8 + i] / st:.0f} ({c[8 + i] / tot:.0%})" for i, n in enumerate(names)), flush=True)
+nb = max(sum(c[19:23]), 1)
+print(f"epilogue blocks {nb} ({nb / st:.2f} per stage): above counter width {c[19] / nb:.1%}, "
+      f"prefilter empty {c[20] / nb:.1%}, exact empty {c[21] / nb:.1%}, with candidates {c[22] / nb:.1%}; "
+      f"extraction rounds {c[23]} ({c[23] / max(c[22], 1):.2f} per candidate block)", flush=True)
