@@ -666,17 +666,18 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
   bool hold = oexp != 0u, abort = false;
   uint32_t dsum = 0;
   int snap = Q.n;
+  // prefilter masks of the 8 segments, lane s: the nibble bits at or above
+  // the highest power of two <= m_s (0 when m_s > 15: no 4-bit count reaches it)
+  const uint32_t mu = static_cast<uint32_t>(mseg);
+  const uint32_t pmv = mu > 15u ? 0u : (0x10u - (0x80000000u >> __builtin_clz(mu | 1u))) * 0x11111111u;
   auto block = [&](uint4 a, int blk) {
-    const uint32_t m = static_cast<uint32_t>(readlane(mseg, blk));
-    if (m > 15u || !((bmask >> blk) & 1u)) {   // no 4-bit count reaches m / overflowed half
-      if (kProfile) ++ra.bk[0];
-      return;
-    }
-    const uint32_t pm = (0x10u - (0x80000000u >> __builtin_clz(m))) * 0x11111111u;
+    if (!((bmask >> blk) & 1u)) return;            // overflowed half (optimistic pass)
+    const uint32_t pm = static_cast<uint32_t>(readlane(pmv, blk));
     if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) {
       if (kProfile) ++ra.bk[1];
       return;
     }
+    const uint32_t m = static_cast<uint32_t>(readlane(mseg, blk));
     // target (8*dw + nib) of this lane's 32 -> bit 4*nib + 3 - dw
     // per-nibble flags (bit 3): nibble >= m, 1 <= m <= 15 (no carry leaves a
     // nibble: low3 + 16 - m <= 14); m is wave-uniform, so one branch per block
@@ -829,17 +830,16 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
   const int xr = x_lab - tile_base;
   const bool xin = static_cast<uint32_t>(xr) < kW1;     // the source is a target of this tile
   const int xrel = xin ? xr : 0;
+  // prefilter masks of the 8 segments, lane s (as in epi1_u4; 0 when m_s > 255)
+  const uint32_t mu = static_cast<uint32_t>(mseg);
+  const uint32_t pmv = mu > 255u ? 0u : (0x100u - (0x80000000u >> __builtin_clz(mu | 1u))) * 0x01010101u;
   auto block = [&](uint4 a, int blk) {
-    const uint32_t m = static_cast<uint32_t>(readlane(mseg, blk));
-    if (m > 255u) {                               // no u8 count reaches m
-      if (kProfile) ++ra.bk[0];
-      return;
-    }
-    const uint32_t pm = (0x100u - (0x80000000u >> __builtin_clz(m))) * 0x01010101u;
+    const uint32_t pm = static_cast<uint32_t>(readlane(pmv, blk));
     if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) {
       if (kProfile) ++ra.bk[1];
       return;
     }
+    const uint32_t m = static_cast<uint32_t>(readlane(mseg, blk));
     uint32_t F;
     if (m <= 128u) {
       const uint32_t kA = (128u - m) * 0x01010101u;
