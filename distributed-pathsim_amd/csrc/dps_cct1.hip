@@ -900,9 +900,10 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
 // that venue's lane with two independent bpermutes.  (kSel swept on the full
 // config3 launch: 4 / 8 / 16 = 72.3 / 73.2 / 73.8 ms in round 3; with the
 // round-4 register allocation 1 / 2 / 3 / 4 / 6 = 66.45 / 66.5 / 66.65 / 66.86
-// / 67.3 ms, profiles/r04/ab/ab4n, ab4o.)
+// / 67.3 ms, profiles/r04/ab/ab4n, ab4o; round 5, after the epilogue and
+// flush changes: 1 / 2 / 3 = 59.9 / 60.2 / 60.3 ms, profiles/r05/kab/ab5g.)
 #ifndef DPS_KSEL
-#define DPS_KSEL 2
+#define DPS_KSEL 1
 #endif
 // The chunk a dead lane (past the stage's last chunk) loads instead of a real
 // one: lane L's 16-bit entries all address accumulator dword L (h = L << 5 in
