@@ -364,6 +364,95 @@ __global__ __launch_bounds__(kWideBlock) void k_col_sums_wide(const int64_t* __r
   }
 }
 
+// Column sums for many mids without re-reading C per mid range (round 5):
+// the entries are first bucketed by mid range (kWideMids mids each) -- a
+// per-block LDS count of each range's entries, one exclusive scan of the
+// [range][block] counts, and a scatter of packed (local mid | author flag,
+// C) pairs with LDS cursors -- then every range is reduced from its own
+// bucket in LDS as in k_col_sums_wide.  Three reads and one write of 8 B per
+// entry instead of one 4 B read per entry per range (config4: 17 ranges).
+constexpr int kCsBlocks = 1024;       // blocks of the count / scatter passes
+constexpr int kCsMaxRanges = 4096;    // n_mids <= kCsMaxRanges * kWideMids
+constexpr uint32_t kCsAuthor = 0x80000000u;
+
+__device__ __forceinline__ void cs_chunk(int64_t nnz, int64_t& j0, int64_t& j1) {
+  const int64_t per = (nnz + gridDim.x - 1) / gridDim.x;
+  j0 = min(static_cast<int64_t>(blockIdx.x) * per, nnz);
+  j1 = min(j0 + per, nnz);
+}
+
+__global__ __launch_bounds__(kBlock) void k_cs_count(const int64_t* __restrict__ c_ptr,
+                                                     const int32_t* __restrict__ c_col,
+                                                     int64_t n_rows, int n_ranges,
+                                                     uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[kCsMaxRanges];
+  for (int r = threadIdx.x; r < n_ranges; r += kBlock) h[r] = 0;
+  __syncthreads();
+  const int64_t b0 = c_ptr[0];
+  int64_t j0, j1;
+  cs_chunk(c_ptr[n_rows] - b0, j0, j1);
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += kBlock)
+    atomicAdd(&h[c_col[b0 + j] / kWideMids], 1u);
+  __syncthreads();
+  for (int r = threadIdx.x; r < n_ranges; r += kBlock) cnt[static_cast<int64_t>(r) * gridDim.x + blockIdx.x] = h[r];
+}
+
+__global__ __launch_bounds__(kBlock) void k_cs_scatter(const int64_t* __restrict__ c_ptr,
+                                                       const int32_t* __restrict__ c_col,
+                                                       const int32_t* __restrict__ c_val,
+                                                       int64_t n_rows, int64_t n_count_rows,
+                                                       int n_ranges, const int64_t* __restrict__ off,
+                                                       int64_t cap, uint2* __restrict__ pairs) {
+  __shared__ unsigned long long cur[kCsMaxRanges];
+  for (int r = threadIdx.x; r < n_ranges; r += kBlock)
+    cur[r] = static_cast<unsigned long long>(off[static_cast<int64_t>(r) * gridDim.x + blockIdx.x]);
+  __syncthreads();
+  const int64_t b0 = c_ptr[0];
+  const int64_t ncnt = c_ptr[n_count_rows] - b0;
+  int64_t j0, j1;
+  cs_chunk(c_ptr[n_rows] - b0, j0, j1);
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += kBlock) {
+    const int32_t v = c_col[b0 + j];
+    const int r = v / kWideMids;
+    const unsigned long long pos = atomicAdd(&cur[r], 1ull);
+    if (pos < static_cast<unsigned long long>(cap))
+      pairs[pos] = make_uint2(static_cast<uint32_t>(v - r * kWideMids) | (j < ncnt ? kCsAuthor : 0u),
+                            static_cast<uint32_t>(c_val[b0 + j]));
+  }
+}
+
+// block (x, y): its share of range y's bucket [off[y * nb], off[(y + 1) * nb]).
+__global__ __launch_bounds__(kWideBlock) void k_cs_range(const uint2* __restrict__ pairs,
+                                                         const int64_t* __restrict__ off, int nb,
+                                                         const int64_t* __restrict__ c_ptr,
+                                                         int64_t n_rows, int64_t cap, int64_t n_mids,
+                                                         unsigned long long* __restrict__ s,
+                                                         unsigned* __restrict__ n_v) {
+  __shared__ unsigned long long h[kWideMids];
+  __shared__ unsigned hc[kWideMids];
+  const int64_t m0 = static_cast<int64_t>(blockIdx.y) * kWideMids;
+  const int m = static_cast<int>(min(static_cast<int64_t>(kWideMids), n_mids - m0));
+  for (int i = threadIdx.x; i < m; i += kWideBlock) { h[i] = 0; hc[i] = 0; }
+  __syncthreads();
+  const int64_t total = c_ptr[n_rows] - c_ptr[0];
+  const int64_t a = min(off[static_cast<int64_t>(blockIdx.y) * nb], cap);
+  const int64_t b = min(blockIdx.y + 1 < gridDim.y ? off[static_cast<int64_t>(blockIdx.y + 1) * nb] : total, cap);
+  const int64_t per = (b - a + gridDim.x - 1) / gridDim.x;
+  const int64_t q0 = a + min(static_cast<int64_t>(blockIdx.x) * per, b - a);
+  const int64_t q1 = min(q0 + per, b);
+  for (int64_t q = q0 + threadIdx.x; q < q1; q += kWideBlock) {
+    const uint2 e = pairs[q];
+    const uint32_t d = e.x & ~kCsAuthor;
+    atomicAdd(&h[d], static_cast<unsigned long long>(e.y));
+    if (n_v && (e.x & kCsAuthor)) atomicAdd(&hc[d], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < m; i += kWideBlock) {
+    if (h[i]) atomicAdd(&s[m0 + i], h[i]);
+    if (n_v && hc[i]) atomicAdd(&n_v[m0 + i], hc[i]);
+  }
+}
+
 __host__ __forceinline__ dim3 col_sums_wide_grid(int64_t n_mids) {
   const unsigned ny = static_cast<unsigned>((n_mids + kWideMids - 1) / kWideMids);
   const unsigned nx = ny >= 512 ? 1u : 512u / ny;
@@ -1424,13 +1513,32 @@ int dps_global_walks(const int64_t* c_ptr, const int32_t* c_col, const int32_t* 
   return DPS_OK;
 }
 
+size_t dps_walks_workspace_size(int64_t nnz_cap, int64_t n_mids) {
+  if (n_mids <= kSumLds || nnz_cap <= 0) return 256;
+  const int64_t nr = (n_mids + kWideMids - 1) / kWideMids;
+  const int64_t m = nr * kCsBlocks;
+  return align_up(static_cast<size_t>(m) * sizeof(uint32_t)) +
+         align_up(static_cast<size_t>(m) * sizeof(int64_t)) + scan_workspace_size(m) +
+         align_up(static_cast<size_t>(nnz_cap) * sizeof(uint2)) + 256;
+}
+
 int dps_walks_fused(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
                     int64_t n_rows, int64_t n_authors, int64_t n_mids, int64_t* s,
                     uint32_t* n_v, int64_t* g, int64_t* diag, int64_t* terms, int64_t* stats,
                     void* stream) {
+  return dps_walks_fused_ws(c_ptr, c_col, c_val, n_rows, n_authors, n_mids, s, n_v, g, diag,
+                            terms, stats, 0, nullptr, 0, stream);
+}
+
+int dps_walks_fused_ws(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                       int64_t n_rows, int64_t n_authors, int64_t n_mids, int64_t* s,
+                       uint32_t* n_v, int64_t* g, int64_t* diag, int64_t* terms, int64_t* stats,
+                       int64_t nnz_cap, void* ws, size_t ws_bytes, void* stream) {
   DPS_REQUIRE(n_rows >= 0 && n_authors >= 0 && n_authors <= n_rows && n_mids >= 0,
               DPS_ERR_INVALID, "bad sizes");
   DPS_REQUIRE(c_ptr && g && (n_mids == 0 || (s && n_v)), DPS_ERR_INVALID, "null array");
+  DPS_REQUIRE(n_mids <= static_cast<int64_t>(kCsMaxRanges) * kWideMids || ws == nullptr,
+              DPS_ERR_INVALID, "too many mids for the bucketed column sums");
   auto st = static_cast<hipStream_t>(stream);
   {
     FillSet fs;   // stats, s and n_v zeroed in one launch
@@ -1442,7 +1550,34 @@ int dps_walks_fused(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c
     DPS_HIP_RET(fill_set(fs, st));
   }
   if (n_mids > 0) {
-    if (n_rows > 0 && n_mids > kSumLds) {
+    if (n_rows > 0 && n_mids > kSumLds && ws != nullptr && nnz_cap > 0) {
+      // bucketed by mid range (nnz_cap >= nnz C: the caller's bound, as for
+      // the SpGEMM output; the scatter never writes past it)
+      DPS_REQUIRE(ws_bytes >= dps_walks_workspace_size(nnz_cap, n_mids), DPS_ERR_WORKSPACE,
+                  "walks workspace too small");
+      DPS_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 256 == 0, DPS_ERR_WORKSPACE,
+                  "workspace not 256-byte aligned");
+      const int nr = static_cast<int>((n_mids + kWideMids - 1) / kWideMids);
+      const int64_t m = static_cast<int64_t>(nr) * kCsBlocks;
+      Carve c(ws, ws_bytes);
+      uint32_t* cnt = c.take<uint32_t>(m);
+      int64_t* off = c.take<int64_t>(m);
+      const size_t sws_bytes = scan_workspace_size(m);
+      void* sws = c.take<char>(sws_bytes);
+      uint2* pairs = c.take<uint2>(nnz_cap);
+      DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "walks workspace carve failed");
+      k_cs_count<<<kCsBlocks, kBlock, 0, st>>>(c_ptr, c_col, n_rows, nr, cnt);
+      DPS_LAUNCHED();
+      DPS_HIP_RET(scan_exclusive<uint32_t>(cnt, off, m, sws, sws_bytes, st));
+      k_cs_scatter<<<kCsBlocks, kBlock, 0, st>>>(c_ptr, c_col, c_val, n_rows, n_authors, nr, off,
+                                                 nnz_cap, pairs);
+      DPS_LAUNCHED();
+      const unsigned nx = nr >= 512 ? 1u : 512u / static_cast<unsigned>(nr);
+      k_cs_range<<<dim3(nx, static_cast<unsigned>(nr)), kWideBlock, 0, st>>>(
+          pairs, off, kCsBlocks, c_ptr, n_rows, nnz_cap, n_mids,
+          reinterpret_cast<unsigned long long*>(s), n_v);
+      DPS_LAUNCHED();
+    } else if (n_rows > 0 && n_mids > kSumLds) {
       k_col_sums_wide<<<col_sums_wide_grid(n_mids), kWideBlock, 0, st>>>(
           c_ptr, c_col, c_val, n_rows, n_mids, reinterpret_cast<unsigned long long*>(s), n_authors,
           n_v);

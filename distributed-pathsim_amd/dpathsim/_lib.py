@@ -73,6 +73,9 @@ SIGNATURES = {
     "dps_row_work": (C.c_int, [_p, _p, _i64, _i64, _p, _p, _p]),
     "dps_col_sums": (C.c_int, [_p, _p, _p, _i64, _i64, _p, _p]),
     "dps_walks_fused": (C.c_int, [_p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p]),
+    "dps_walks_fused_ws": (C.c_int, [_p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _i64, _p,
+                                     _sz, _p]),
+    "dps_walks_workspace_size": (C.c_size_t, [_i64, _i64]),
     "dps_target_order_workspace_size": (_sz, [_i64]),
     "dps_target_order": (C.c_int, [_p, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "dps_ct_tiles_workspace_size": (_sz, [_i64, _i64, _i32]),

@@ -275,8 +275,11 @@ class PathSimEngine:
             diag = self._empty(NA, torch.int64)
             terms = self._empty(NA, torch.int64)
             stats = self._empty(_lib.STATS_LEN, torch.int64)
-            _lib.call("dps_walks_fused", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NR, NA, NV,
-                      _ptr(s), _ptr(n_v), _ptr(g), _ptr(diag), _ptr(terms), _ptr(stats), st)
+            wws = self._ws(_lib.size("dps_walks_workspace_size", cap, NV))
+            _lib.call("dps_walks_fused_ws", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), NR, NA, NV,
+                      _ptr(s), _ptr(n_v), _ptr(g), _ptr(diag), _ptr(terms), _ptr(stats), cap,
+                      _ptr(wws), wws.numel(), st)
+            del wws
             mark("walks")
             # the per-author denominator term of the score
             den = g if self.denominator == "rowsum" else diag

@@ -236,6 +236,15 @@ int dps_walks_fused(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c
                     int64_t n_rows, int64_t n_authors, int64_t n_mids, int64_t* s,
                     uint32_t* n_v, int64_t* g, int64_t* diag, int64_t* terms, int64_t* stats,
                     void* stream);
+/* The same with a workspace (dps_walks_workspace_size(nnz_cap, n_mids) bytes,
+ * 256-byte aligned; nnz_cap >= nnz C, e.g. the SpGEMM output capacity): with
+ * more mids than one LDS range the column sums bucket C's entries by mid range
+ * once instead of re-reading C per range.  ws == NULL: as dps_walks_fused. */
+size_t dps_walks_workspace_size(int64_t nnz_cap, int64_t n_mids);
+int dps_walks_fused_ws(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                       int64_t n_rows, int64_t n_authors, int64_t n_mids, int64_t* s,
+                       uint32_t* n_v, int64_t* g, int64_t* diag, int64_t* terms, int64_t* stats,
+                       int64_t nnz_cap, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * A5 operand layout, step 1: target relabeling (a pure layout choice; results

@@ -8,8 +8,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("n_mids", [500, 20_000, 40_000])
 def test_fused_walks_match_separate_entry_points(n_mids):
-    """500 mids: the LDS column sums of one range; 20k / 40k: the range-blocked
-    wide kernel (mids over several 12288-mid LDS ranges, the last one partial)."""
+    """500 mids: the LDS column sums of one range; 20k / 40k: mids over several
+    12288-mid LDS ranges, the last one partial -- the engine's bucketed column
+    sums (dps_walks_fused_ws) and the per-range re-reading kernel
+    (dps_walks_fused without a workspace) must agree with each other and the
+    oracle."""
     import torch
     import pathsim_oracle as po
     from dpathsim import _lib
@@ -37,3 +40,14 @@ def test_fused_walks_match_separate_entry_points(n_mids):
     n_v = np.bincount(cc[: cp[na]], minlength=nv)
     expect = np.add.reduceat(n_v[cc[: cp[na]]], cp[:na]) * (np.diff(cp[: na + 1]) > 0)
     assert np.array_equal(terms.cpu().numpy(), expect)
+    # the same pass without a workspace (per-range re-reads for wide mids)
+    s2 = torch.empty(nv, dtype=torch.int64, device="cuda")
+    nv2 = torch.empty(nv, dtype=torch.int32, device="cuda")
+    g2 = torch.empty(na, dtype=torch.int64, device="cuda")
+    t2 = torch.empty(na, dtype=torch.int64, device="cuda")
+    _lib.call("dps_walks_fused", d["c_ptr"].data_ptr(), d["c_col"].data_ptr(), d["c_val"].data_ptr(),
+              nr, na, nv, s2.data_ptr(), nv2.data_ptr(), g2.data_ptr(), None, t2.data_ptr(), None, st)
+    assert torch.equal(s2, d["s"][:nv])
+    assert torch.equal(g2, d["g"][:na])
+    assert torch.equal(t2, d["row_terms"][:na])
+    assert np.array_equal(nv2.cpu().numpy(), n_v)
