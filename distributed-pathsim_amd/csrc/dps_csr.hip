@@ -23,7 +23,10 @@ __device__ __forceinline__ int64_t bound_from(const int64_t* dev, int64_t host) 
 // ---------------------------------------------------------------------------
 // A2: typed incidence extraction (DPathSim_APVPA.py:78-84).  Wave-aggregated
 // atomic append: one atomic per wave per output list.
-constexpr int kExtractPer = 16;   // edges per lane per wave chunk
+#ifndef DPS_EXTRACT_PER
+#define DPS_EXTRACT_PER 16
+#endif
+constexpr int kExtractPer = DPS_EXTRACT_PER;   // edges per lane per wave chunk (<= 32)
 
 __global__ __launch_bounds__(kBlock) void k_extract(
     const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
