@@ -200,6 +200,11 @@ void orc_topk_rows(const orc_state* st, const int64_t* rows, int64_t n_rows, int
         acc[y] = 0;
         if (y == x) continue;
         const int64_t den = dx + den_of[y];
+        /* A full list's k-th score bounds the division from below: when
+         * 2m < kth * den * (1 - 2^-40) (each side exact or within 2^-52), the
+         * rounded quotient is below kth by many ulps and cannot beat it --
+         * the division is skipped, the result is the same. */
+        if (filled == k && den && (double)(2 * m) < ts[k - 1] * (double)den * (1.0 - 0x1p-40)) continue;
         const double sc = den ? (double)(2 * m) / (double)den : 0.0;
         if (filled == k && !better(sc, y, ts[k - 1], ty[k - 1])) continue;
         int pos = filled < k ? filled : k - 1;
