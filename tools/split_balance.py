@@ -5,7 +5,11 @@ engine's split path with a recording stand-in for the all-gather); then each
 rank's whole build is timed (events, eng.build) with an all-gather that copies
 the recorded slices into place (a device copy of the gathered bytes: the
 receive side's HBM writes; the xGMI transfer itself is modelled below), and the
-hot kernel over each rank's row shard (bench.py's plan).  Predicted step =
+hot kernel over each rank's row shard (bench.py's plan); and (round 5) the
+replicated build and the shard's top-k enqueued back to back in one event
+span, as bench.py's step runs them, plus the result gather to rank 0 over one
+xGMI link per peer ("joint_replicated_speedup" against the same span at
+N = 1).  Predicted step =
 max over ranks of (build + shard kernel) + the modelled all-gather
 (gathered bytes * (N-1)/N / XGMI_GBPS, default 150 GB/s = one xGMI link's worth:
 every rank sends its slice to N-1 peers).  Prints JSON lines."""
@@ -66,7 +70,14 @@ ref = build_engine(t)
 ref.topk(k, 0, 20000)
 full = ev_time(lambda: ref.topk(k), 2)
 build1 = ev_time(lambda: ref.build(check=False))
-print(json.dumps({"config": cfg, "world": 1, "hot_ms": full, "build_ms": build1}), flush=True)
+# the step as bench.py runs it: build and top-k enqueued back to back, one
+# event span (the host's enqueue of the top-k overlaps the build's GPU time)
+joint1 = ev_time(lambda: (ref.build(check=False), ref.topk(k)), 2)
+print(json.dumps({"config": cfg, "world": 1, "hot_ms": full, "build_ms": build1,
+                  "joint_step_ms": joint1}), flush=True)
+# result gather to rank 0 (bench's packed 8-byte words): each peer's rows over
+# its own xGMI link to rank 0
+RES_B = 8 * k
 for world in (2, 4, 8):
     # record every rank's slices with the exact plan capacities
     sent = []
@@ -103,14 +114,20 @@ for world in (2, 4, 8):
         b_ms = ev_time(step)
         a, b = bounds[r]
         s_ms = ev_time(lambda a=a, b=b: ref.topk(k, a, b), 2)
-        rows.append((b_ms, s_ms))
+        j_ms = ev_time(lambda a=a, b=b: (ref.build(check=False), ref.topk(k, a, b)), 2)
+        rows.append((b_ms, s_ms, j_ms, b - a))
         del e
         torch.cuda.empty_cache()
-    step_ms = max(b + s for b, s in rows) + ag_ms
-    repl_ms = max(s for _, s in rows) + build1
+    step_ms = max(b + s for b, s, _, _ in rows) + ag_ms
+    repl_ms = max(s for _, s, _, _ in rows) + build1
+    res_ms = max(n for _, _, _, n in rows) * RES_B / (XGMI * 1e9) * 1e3
+    joint_ms = max(j for _, _, j, _ in rows) + res_ms
     print(json.dumps({"config": cfg, "world": world,
-                      "build_ms": [round(b, 3) for b, _ in rows],
-                      "shard_ms": [round(s, 2) for _, s in rows],
+                      "build_ms": [round(b, 3) for b, _, _, _ in rows],
+                      "shard_ms": [round(s, 2) for _, s, _, _ in rows],
+                      "joint_replicated_step_ms": [round(j, 2) for _, _, j, _ in rows],
+                      "result_gather_model_ms": res_ms,
+                      "joint_replicated_speedup": joint1 / joint_ms,
                       "gathered_MB": gbytes / 1e6, "allgather_model_ms": ag_ms,
                       "predicted_step_ms": step_ms,
                       "predicted_speedup": (full + build1) / step_ms,
