@@ -728,7 +728,9 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
       }
     }
   };
-#pragma unroll 1
+  // two trips per loop iteration (round 5: 58.7 vs 60.0 ms on the full
+  // config3 launch with one; still one 1 KiB block read per trip)
+#pragma unroll 2
   for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4 * kEpi1) {
     uint4 a[kEpi1];
 #pragma unroll
@@ -879,7 +881,7 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
       if (Q.n >= kWave) vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
     }
   };
-#pragma unroll 1
+#pragma unroll 2
   for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4 * kEpi1) {
     uint4 a[kEpi1];
 #pragma unroll
