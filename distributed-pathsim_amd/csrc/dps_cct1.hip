@@ -881,7 +881,8 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
       if (Q.n >= kWave) vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
     }
   };
-#pragma unroll 2
+  // four trips per loop iteration (round 5: 58.2 vs 58.8 ms with two)
+#pragma unroll 4
   for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4 * kEpi1) {
     uint4 a[kEpi1];
 #pragma unroll
