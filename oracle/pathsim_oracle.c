@@ -161,6 +161,87 @@ static int better(double s1, int32_t y1, double s2, int32_t y2) {
   return s1 > s2 || (s1 == s2 && y1 < y2);
 }
 
+/* One source row x: M[x, .] accumulated in acc (type T, all zero on entry
+ * and on exit), ranked into the k slots at out_*[o ..].  A full list's k-th
+ * score bounds the division from below: when 2m < kth * den * (1 - 2^-40)
+ * (each side exact or within 2^-52), the rounded quotient is below kth by
+ * many ulps and cannot beat it -- the division is skipped, the result is the
+ * same. */
+#define ORC_ROW_TOPK(NAME, T)                                                              \
+  static void NAME(const orc_state* st, const int64_t* den_of, int64_t na, int64_t x,      \
+                   int k, T* acc, int32_t* touched, double* ts, int32_t* ty, int64_t* tm,  \
+                   int32_t* out_idx, int64_t* out_cnt, double* out_score, int64_t o) {     \
+    int64_t nt = 0;                                                                         \
+    for (int64_t j = st->c_ptr[x]; j < st->c_ptr[x + 1]; ++j) {                            \
+      const int32_t v = st->c_col[j];                                                       \
+      const T cx = (T)st->c_val[j];                                                         \
+      for (int64_t q = st->t_ptr[v]; q < st->t_ptr[v + 1]; ++q) {                          \
+        const int32_t y = st->t_row[q];                                                     \
+        if (acc[y] == 0) touched[nt++] = y;                                                 \
+        acc[y] += cx * (T)st->t_val[q];                                                     \
+      }                                                                                     \
+    }                                                                                       \
+    int filled = 0;                                                                         \
+    const int64_t dx = den_of[x];                                                           \
+    for (int64_t t = 0; t < nt; ++t) {                                                      \
+      const int32_t y = touched[t];                                                         \
+      const int64_t m = (int64_t)acc[y];                                                    \
+      acc[y] = 0;                                                                           \
+      if (y == x) continue;                                                                 \
+      const int64_t den = dx + den_of[y];                                                   \
+      if (filled == k && den && (double)(2 * m) < ts[k - 1] * (double)den * (1.0 - 0x1p-40)) \
+        continue;                                                                           \
+      const double sc = den ? (double)(2 * m) / (double)den : 0.0;                          \
+      if (filled == k && !better(sc, y, ts[k - 1], ty[k - 1])) continue;                    \
+      int pos = filled < k ? filled : k - 1;                                                \
+      while (pos > 0 && better(sc, y, ts[pos - 1], ty[pos - 1])) {                          \
+        ts[pos] = ts[pos - 1]; ty[pos] = ty[pos - 1]; tm[pos] = tm[pos - 1];                \
+        --pos;                                                                              \
+      }                                                                                     \
+      ts[pos] = sc; ty[pos] = y; tm[pos] = m;                                               \
+      if (filled < k) ++filled;                                                             \
+    }                                                                                       \
+    /* zero-score fill by ascending target index, self and ranked excluded */              \
+    int64_t want = (na - 1) < k ? (na - 1) : k;                                             \
+    for (int64_t y = 0; filled < want && y < na; ++y) {                                     \
+      if (y == x) continue;                                                                 \
+      int dup = 0;                                                                          \
+      for (int q = 0; q < filled; ++q) if (ty[q] == y && ts[q] > 0.0) { dup = 1; break; }   \
+      if (dup) continue;                                                                    \
+      ts[filled] = 0.0; ty[filled] = (int32_t)y; tm[filled] = 0; ++filled;                  \
+    }                                                                                       \
+    for (int q = 0; q < k; ++q) {                                                           \
+      if (q < filled) {                                                                     \
+        out_idx[o + q] = ty[q]; out_cnt[o + q] = tm[q]; out_score[o + q] = ts[q];           \
+      } else {                                                                              \
+        out_idx[o + q] = -1; out_cnt[o + q] = 0; out_score[o + q] = 0.0;                    \
+      }                                                                                     \
+    }                                                                                       \
+  }
+ORC_ROW_TOPK(row_topk_i64, int64_t)
+ORC_ROW_TOPK(row_topk_i32, int32_t)
+
+/* Every M[x, y] of the author rows fits 31 bits: sum_{v in x} C[x,v] *
+ * max_y C[y,v] < 2^31 for every x.  Then the accumulators are int32 (half the
+ * bytes of the per-thread dense row: the scatter is a random walk over it). */
+static int fits_i32(const orc_state* st) {
+  const int64_t nv = st->n_mids;
+  int64_t* colmax = (int64_t*)calloc((size_t)nv + 1, sizeof(int64_t));
+  for (int64_t v = 0; v < nv; ++v)
+    for (int64_t q = st->t_ptr[v]; q < st->t_ptr[v + 1]; ++q)
+      if (st->t_val[q] > colmax[v]) colmax[v] = st->t_val[q];
+  int ok = 1;
+  for (int64_t x = 0; ok && x < st->n_authors; ++x) {
+    int64_t b = 0;
+    for (int64_t j = st->c_ptr[x]; j < st->c_ptr[x + 1]; ++j) {
+      b += (int64_t)st->c_val[j] * colmax[st->c_col[j]];
+      if (b >= ((int64_t)1 << 31)) { ok = 0; break; }
+    }
+  }
+  free(colmax);
+  return ok;
+}
+
 /* Top-k of source rows: rows[i] (i < n_rows) if rows != NULL, else row_begin + i.
  * use_diag != 0 replaces the reference's row-sum denominator g[x] + g[y]
  * (DPathSim_APVPA.py:51-52 with :70-88) by the textbook M[x,x] + M[y,y]. */
@@ -169,12 +250,13 @@ void orc_topk_rows(const orc_state* st, const int64_t* rows, int64_t n_rows, int
                    int use_diag) {
   const int64_t na = st->n_authors;
   const int64_t* den_of = use_diag ? st->diag : st->g;
+  const int narrow = fits_i32(st);
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
 #pragma omp parallel
   {
-    int64_t* acc = (int64_t*)calloc((size_t)na + 1, sizeof(int64_t));
+    void* acc = calloc((size_t)na + 1, narrow ? sizeof(int32_t) : sizeof(int64_t));
     int32_t* touched = (int32_t*)malloc(sizeof(int32_t) * ((size_t)na + 1));
     double* ts = (double*)malloc(sizeof(double) * (size_t)k);
     int32_t* ty = (int32_t*)malloc(sizeof(int32_t) * (size_t)k);
@@ -182,56 +264,12 @@ void orc_topk_rows(const orc_state* st, const int64_t* rows, int64_t n_rows, int
 #pragma omp for schedule(dynamic, 16)
     for (int64_t i = 0; i < n_rows; ++i) {
       const int64_t x = rows ? rows[i] : row_begin + i;
-      int64_t nt = 0;
-      for (int64_t j = st->c_ptr[x]; j < st->c_ptr[x + 1]; ++j) {
-        const int32_t v = st->c_col[j];
-        const int64_t cx = st->c_val[j];
-        for (int64_t q = st->t_ptr[v]; q < st->t_ptr[v + 1]; ++q) {
-          const int32_t y = st->t_row[q];
-          if (acc[y] == 0) touched[nt++] = y;
-          acc[y] += cx * st->t_val[q];
-        }
-      }
-      int filled = 0;
-      const int64_t dx = den_of[x];
-      for (int64_t t = 0; t < nt; ++t) {
-        const int32_t y = touched[t];
-        const int64_t m = acc[y];
-        acc[y] = 0;
-        if (y == x) continue;
-        const int64_t den = dx + den_of[y];
-        /* A full list's k-th score bounds the division from below: when
-         * 2m < kth * den * (1 - 2^-40) (each side exact or within 2^-52), the
-         * rounded quotient is below kth by many ulps and cannot beat it --
-         * the division is skipped, the result is the same. */
-        if (filled == k && den && (double)(2 * m) < ts[k - 1] * (double)den * (1.0 - 0x1p-40)) continue;
-        const double sc = den ? (double)(2 * m) / (double)den : 0.0;
-        if (filled == k && !better(sc, y, ts[k - 1], ty[k - 1])) continue;
-        int pos = filled < k ? filled : k - 1;
-        while (pos > 0 && better(sc, y, ts[pos - 1], ty[pos - 1])) {
-          ts[pos] = ts[pos - 1]; ty[pos] = ty[pos - 1]; tm[pos] = tm[pos - 1];
-          --pos;
-        }
-        ts[pos] = sc; ty[pos] = y; tm[pos] = m;
-        if (filled < k) ++filled;
-      }
-      /* zero-score fill by ascending target index, self and ranked excluded */
-      int64_t want = (na - 1) < k ? (na - 1) : k;
-      for (int64_t y = 0; filled < want && y < na; ++y) {
-        if (y == x) continue;
-        int dup = 0;
-        for (int q = 0; q < filled; ++q) if (ty[q] == y && ts[q] > 0.0) { dup = 1; break; }
-        if (dup) continue;
-        ts[filled] = 0.0; ty[filled] = (int32_t)y; tm[filled] = 0; ++filled;
-      }
-      const int64_t o = i * k;
-      for (int q = 0; q < k; ++q) {
-        if (q < filled) {
-          out_idx[o + q] = ty[q]; out_cnt[o + q] = tm[q]; out_score[o + q] = ts[q];
-        } else {
-          out_idx[o + q] = -1; out_cnt[o + q] = 0; out_score[o + q] = 0.0;
-        }
-      }
+      if (narrow)
+        row_topk_i32(st, den_of, na, x, k, (int32_t*)acc, touched, ts, ty, tm, out_idx, out_cnt,
+                     out_score, i * k);
+      else
+        row_topk_i64(st, den_of, na, x, k, (int64_t*)acc, touched, ts, ty, tm, out_idx, out_cnt,
+                     out_score, i * k);
     }
     free(acc); free(touched); free(ts); free(ty); free(tm);
   }
