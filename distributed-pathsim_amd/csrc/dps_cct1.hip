@@ -728,9 +728,12 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
       }
     }
   };
-  // two trips per loop iteration (round 5: 58.7 vs 60.0 ms on the full
-  // config3 launch with one; still one 1 KiB block read per trip)
-#pragma unroll 2
+  // two trips per loop iteration for the top-10 instantiation, four for the
+  // two-register top-k (round 5: config3 58.7 vs 60.0 ms with one trip, 58.1
+  // vs 58.55 with four; config5 609 vs 624 ms with four instead of two;
+  // still one 1 KiB block read per trip)
+  constexpr int kTrips = KPL == 1 ? 2 : 4;
+#pragma unroll kTrips
   for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4 * kEpi1) {
     uint4 a[kEpi1];
 #pragma unroll
