@@ -147,6 +147,22 @@ orc_state* orc_create(int64_t n_ap, const int32_t* ap_row, const int32_t* ap_col
 
 int64_t orc_nnz(const orc_state* st) { return st->c_ptr[st->n_authors]; }
 
+/* Test switches (orc_set_flags; 0 = the defaults every caller gets):
+ *   ORC_FORCE_I64  int64 accumulators even when fits_i32 proves int32 suffices;
+ *   ORC_NO_SKIP    no division-skip bound (every candidate is divided).
+ * tests/test_oracle.py runs the oracle both ways against the numpy restatement,
+ * so the shortcuts below are checked against the plain algorithm. */
+#define ORC_FORCE_I64 1
+#define ORC_NO_SKIP 2
+static int orc_flags = 0;
+void orc_set_flags(int flags) { orc_flags = flags; }
+int orc_get_flags(void) { return orc_flags; }
+
+static int fits_i32(const orc_state* st);
+
+/* 1 when the top-k runs on int32 accumulators (fits_i32, no ORC_FORCE_I64). */
+int orc_narrow(const orc_state* st) { return !(orc_flags & ORC_FORCE_I64) && fits_i32(st); }
+
 void orc_export(const orc_state* st, int64_t* c_ptr, int32_t* c_col, int32_t* c_val, int64_t* s,
                 int64_t* g) {
   const int64_t nnz = orc_nnz(st);
@@ -183,13 +199,15 @@ static int better(double s1, int32_t y1, double s2, int32_t y2) {
     }                                                                                       \
     int filled = 0;                                                                         \
     const int64_t dx = den_of[x];                                                           \
+    const int skip_ok = !(orc_flags & ORC_NO_SKIP);                                         \
     for (int64_t t = 0; t < nt; ++t) {                                                      \
       const int32_t y = touched[t];                                                         \
       const int64_t m = (int64_t)acc[y];                                                    \
       acc[y] = 0;                                                                           \
       if (y == x) continue;                                                                 \
       const int64_t den = dx + den_of[y];                                                   \
-      if (filled == k && den && (double)(2 * m) < ts[k - 1] * (double)den * (1.0 - 0x1p-40)) \
+      if (skip_ok && filled == k && den &&                                                  \
+          (double)(2 * m) < ts[k - 1] * (double)den * (1.0 - 0x1p-40))                      \
         continue;                                                                           \
       const double sc = den ? (double)(2 * m) / (double)den : 0.0;                          \
       if (filled == k && !better(sc, y, ts[k - 1], ty[k - 1])) continue;                    \
@@ -250,7 +268,7 @@ void orc_topk_rows(const orc_state* st, const int64_t* rows, int64_t n_rows, int
                    int use_diag) {
   const int64_t na = st->n_authors;
   const int64_t* den_of = use_diag ? st->diag : st->g;
-  const int narrow = fits_i32(st);
+  const int narrow = !(orc_flags & ORC_FORCE_I64) && fits_i32(st);
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif

@@ -238,6 +238,10 @@ class COracle:
         lib.orc_topk_rows.argtypes = [P, P, I64, I64, C.c_int, P, P, P, C.c_int, C.c_int]
         lib.orc_diag.argtypes = [P, P]
         lib.orc_destroy.argtypes = [P]
+        lib.orc_set_flags.argtypes = [C.c_int]
+        lib.orc_get_flags.restype = C.c_int
+        lib.orc_narrow.restype = C.c_int
+        lib.orc_narrow.argtypes = [P]
         self._lib = lib
         a = [np.ascontiguousarray(x, dtype=np.int32) for x in (ap_row, ap_col, px_paper, px_mid)]
         self._keep = a
@@ -295,6 +299,17 @@ class COracle:
                                     cnt.ctypes.data, sc.ctypes.data, int(threads),
                                     int(denominator == "diag"))
         return idx, cnt, sc
+
+    # test switches of the C restatement (pathsim_oracle.c: ORC_FORCE_I64,
+    # ORC_NO_SKIP); process-wide, tests restore 0 afterwards
+    FORCE_I64, NO_SKIP = 1, 2
+
+    def set_flags(self, flags):
+        self._lib.orc_set_flags(int(flags))
+
+    def narrow(self):
+        """True when topk() runs on int32 accumulators under the current flags."""
+        return bool(self._lib.orc_narrow(self._st))
 
     def diag(self):
         d = np.zeros(max(self.n_authors, 1), np.int64)

@@ -140,3 +140,92 @@ def test_c_oracle_topk_matches_python_oracle(graph, k):
 def test_networkx_loader_matches_fixture(dblp_small_tuples):
     v, e = po.load_gexf_networkx(REF_GEXF)
     assert (v, e) == dblp_small_tuples
+
+
+# ---- the C oracle's shortcuts against the plain numpy restatement -------------
+# Every full-size GPU parity test compares with the C oracle (COracle), which
+# takes two shortcuts (oracle/pathsim_oracle.c): int32 accumulators when
+# sum_v C[x,v] * max_y C[y,v] < 2^31 for every row, and no division when
+# 2m < kth * den * (1 - 2^-40).  Here both are checked, on and forced off,
+# against allpairs_topk (dense M rows + lexsort, no shortcut) on a 10k-author
+# config3-shaped graph at k = 10 and 100, and on a graph whose path counts need
+# int64 (the wide path taken by the proof, not by a switch).
+def _typed_and_oracles(graph, k):
+    from dpathsim.graph import APVPA
+    t = graph.typed(APVPA)
+    og = po.OracleGraph(graph.vertices(), graph.edges())
+    ref = po.allpairs_topk(og, k, block=256)
+    return t, og, ref
+
+
+def _same(a, b, what):
+    ai, ac, asc = a
+    bi, bc, bsc = b
+    assert np.array_equal(ai, bi), f"{what}: targets differ"
+    assert np.array_equal(ac, bc), f"{what}: path counts differ"
+    assert np.array_equal(asc.view(np.int64), bsc.view(np.int64)), f"{what}: score bits differ"
+
+
+@pytest.fixture(scope="module")
+def config3_10k():
+    from dpathsim.synth import synth_config
+    g = synth_config("config3", scale=0.01)
+    t, og, ref = _typed_and_oracles(g, 100)
+    return t, og, ref
+
+
+@pytest.mark.parametrize("k", [10, 100])
+@pytest.mark.parametrize("flags", [0, 1, 2, 3])
+def test_c_oracle_shortcuts_vs_numpy_config3_10k(config3_10k, k, flags):
+    t, og, ref = config3_10k
+    co = po.COracle.from_typed(t)
+    assert co.n_authors == 10_000
+    try:
+        co.set_flags(flags)
+        assert co.narrow() == (not (flags & po.COracle.FORCE_I64))   # int32 proof holds here
+        got = co.topk(k, threads=4)
+    finally:
+        co.set_flags(0)
+    # (score desc, ordinal asc) is a total order and the zero fill follows it, so
+    # the top-k is the first k columns of the numpy top-100
+    _same(got, tuple(a[:, :k] for a in ref), f"k={k} flags={flags}")
+
+
+def test_c_oracle_wide_counts_vs_numpy():
+    """A graph whose M needs int64 accumulators: few venues, prolific authors
+    (C[x,v] in the thousands), so fits_i32 fails and the int64 path runs with
+    the skip bound on and off."""
+    from dpathsim.synth import synth_dblp
+    g = synth_dblp(400, 600_000, 3, seed=7, author_alpha=1.1, authors_lambda=0.5)
+    t, og, ref = _typed_and_oracles(g, 20)
+    assert int(og.C.max()) > 1000
+    co = po.COracle.from_typed(t)
+    assert not co.narrow()
+    m_max = int((og.C @ og.C.T).max())
+    assert m_max >= 2 ** 31, m_max          # the counts really need 64 bits
+    for flags in (0, po.COracle.NO_SKIP):
+        try:
+            co.set_flags(flags)
+            _same(co.topk(20, threads=4), ref, f"wide flags={flags}")
+        finally:
+            co.set_flags(0)
+
+
+def test_c_oracle_shortcuts_vs_numpy_config3_100k_rows():
+    """config3 at 1/10 scale (100k authors, g up to 3.3e6): 300 random rows plus
+    the 100 largest-g rows at k = 100, shortcuts on and forced off."""
+    from dpathsim.graph import APVPA
+    from dpathsim.synth import synth_config
+    g = synth_config("config3", scale=0.1)
+    og = po.OracleGraph(g.vertices(), g.edges())
+    rng = np.random.default_rng(1)
+    rows = np.unique(np.concatenate([rng.choice(len(og.authors), 300, replace=False),
+                                     np.argsort(og.g)[-100:]]))
+    ref = po.allpairs_topk(og, 100, rows=rows, block=100)
+    co = po.COracle.from_typed(g.typed(APVPA))
+    for flags in (0, po.COracle.FORCE_I64 | po.COracle.NO_SKIP):
+        try:
+            co.set_flags(flags)
+            _same(co.topk_rows(100, rows, threads=4), ref, f"100k flags={flags}")
+        finally:
+            co.set_flags(0)
