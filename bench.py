@@ -65,8 +65,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dpathsim.dist import (RcclComm, TileSplit, gather_topk_compact, max_shard, pack_counts,
-                               shard_edges)
+    from dpathsim.dist import (RcclComm, TileSplit, check_comm_gather, gather_topk_compact,
+                               max_shard, pack_counts, shard_edges)
     from dpathsim.engine import PathSimEngine
     from dpathsim.synth import CONFIGS, synth_config
 
@@ -77,21 +77,43 @@ def main():
     # driver): all ranks on one device, the gather over gloo instead of RCCL
     local = int(os.environ.get("DPATHSIM_BENCH_DEVICE", local))
     backend = os.environ.get("DPATHSIM_BENCH_BACKEND", "rccl")
-    # the top-k gather over RCCL (xGMI): torch.distributed's "nccl" process group
-    # by default; DPATHSIM_BENCH_COMM=capi runs it through libdpathsim's C ABI
-    # (dps_comm_init / dps_gather, gloo as the control plane) instead -- that
-    # path has only run with one rank so far, so it is opt-in
-    comm_kind = os.environ.get("DPATHSIM_BENCH_COMM", "torch")
+    # the top-k gather over RCCL (xGMI): by default through libdpathsim's C ABI
+    # (dps_comm_init / dps_gather = ncclCommInitRank / RCCL send-recv on the
+    # step's stream; gloo is only the control plane: the unique id, barriers,
+    # the timing max) -- SURVEY 8b's dps_gather.  Before the
+    # timed loop rank 0 checks one gather of a known pattern through it in this
+    # process; on a mismatch (or an error) every rank switches to a
+    # torch.distributed nccl group for the gather, in the same process.
+    # DPATHSIM_BENCH_COMM=torch uses the nccl process group from the start.
+    comm_kind = os.environ.get("DPATHSIM_BENCH_COMM", "capi")
     comm = None
+    gather_group = None          # the torch group of the gather when comm is None
+    comm_used = "none" if world == 1 else backend
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
         if backend == "rccl" and comm_kind == "torch":
             dist.init_process_group("nccl", device_id=dev)
+            comm_used = "torch-nccl"
         else:
             dist.init_process_group("gloo")
             if backend == "rccl":
-                comm = RcclComm(device=dev)
+                try:
+                    comm = RcclComm(device=dev)
+                except Exception as e:    # noqa: BLE001 -- falls back below, on every rank
+                    print(f"rank {rank}: dps_comm_init failed ({e})", file=sys.stderr)
+                    comm = None
+                if comm is not None and check_comm_gather(comm, dev):
+                    comm_used = "capi-rccl"
+                else:
+                    if comm is not None:
+                        comm.close()
+                    comm = None
+                    if rank == 0:
+                        print("the C-ABI RCCL gather failed its known-pattern check: "
+                              "using torch.distributed's nccl group", file=sys.stderr)
+                    gather_group = dist.new_group(backend="nccl")
+                    comm_used = "torch-nccl (C-ABI check failed)"
 
     na_cfg, np_cfg, nm_cfg, mp_name, k_cfg = CONFIGS[args.config]
     k = args.k or k_cfg
@@ -112,7 +134,7 @@ def main():
     # on config3 at N = 8) costs more than that saves (tools/split_balance.py,
     # profiles/r05/split_balance.txt)
     if world > 1 and os.environ.get("DPATHSIM_BENCH_SPLIT", "0") == "1":
-        eng.split = TileSplit.from_group(comm=comm, device=dev)
+        eng.split = TileSplit.from_group(group=gather_group, comm=comm, device=dev)
     eng.upload()
 
     eng.build()             # checks the overflow conditions once (one sync); with the
@@ -163,8 +185,9 @@ def main():
             # rank 0 puts the rows in order and rebuilds the fp64 scores from its
             # own g with the same exact division (dps_unpack_gathered)
             pack_counts(out[0], out[1], out=packed)
-            gather_topk_compact(packed, eng.tensor("den")[:NA], NA, world, out=gathered,
-                                bounds=bounds, comm=comm, edges=edges0, result=final)
+            gather_topk_compact(packed, eng.tensor("den")[:NA], NA, world, group=gather_group,
+                                out=gathered, bounds=bounds, comm=comm, edges=edges0,
+                                result=final)
 
     for _ in range(args.warmup):
         step(False)
@@ -364,6 +387,7 @@ def main():
                                  "region starts (the bench contract); SURVEY 8d times them "
                                  "host-resident: that rate is pcie_inclusive.value_incl_h2d*",
                        "parallelism": f"row-shard x{world} (work-balanced, heaviest rows first)",
+                       "gather": comm_used,
                        "build": ("C^T tiles split by target-tile range + all-gather"
                                  if eng.split is not None else "replicated")},
             # bound: the LDS array (the resource the algorithm's unit work lands on;

@@ -698,7 +698,7 @@ using namespace dps;
 
 extern "C" {
 
-size_t dps_cct_topk_workspace_size(void) { return 256; }
+size_t dps_cct_topk_workspace_size(void) { return 512; }
 
 size_t dps_heavy_first_workspace_size(int64_t n_rows) {
   const size_t m = static_cast<size_t>(n_rows > 0 ? n_rows : 1);
@@ -859,7 +859,7 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
     if (const char* ab = std::getenv("DPATHSIM_ABLATE")) p.ablate = std::atoi(ab);
   // word 0: row dequeue counter; words 1-3: the lean kernel's pass / chunk /
   // table-completed candidate counts, word 4 its overflowed optimistic passes
-  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 256 : 8 * sizeof(unsigned long long), st));
+  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 512 : 8 * sizeof(unsigned long long), st));
   // the bench shape (W = 8192, one wave per row) runs the lean kernel
   // (dps_cct1.hip); DPATHSIM_LEAN=0 selects this file's general kernel
   bool lean = (shift == 13 || shift == 14) && nw == 1 && (p.ablate == 0 || p.ablate == 16);

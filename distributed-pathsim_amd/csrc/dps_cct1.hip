@@ -443,6 +443,12 @@ struct RowAux {
   // above the counter width, prefilter empty, exact test empty, with
   // candidates; and candidate extraction rounds
   uint32_t bk[5] = {0, 0, 0, 0, 0};
+  // profiling build: passes by the stage's chunk count (bucket edges 0 / 16 /
+  // 64 / 128 / 192 / 384 / 768), their chunks and their epilogue cycles
+  // (counter[24..31], [32..39], [40..47])
+  uint32_t nqh[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t nqc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t nqe[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int x = 0;               // source row (ordinal)
   int far = INT_MAX;       // sym = 2: targets in tiles >= far may go to records
 };
@@ -673,6 +679,10 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
   auto block = [&](uint4 a, int blk) {
     if (!((bmask >> blk) & 1u)) return;            // overflowed half (optimistic pass)
     const uint32_t pm = static_cast<uint32_t>(readlane(pmv, blk));
+    if (kProfile && pm == 0u) {                    // threshold above the counter width
+      ++ra.bk[0];
+      return;
+    }
     if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) {
       if (kProfile) ++ra.bk[1];
       return;
@@ -840,6 +850,10 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
   const uint32_t pmv = mu > 255u ? 0u : (0x100u - (0x80000000u >> __builtin_clz(mu | 1u))) * 0x01010101u;
   auto block = [&](uint4 a, int blk) {
     const uint32_t pm = static_cast<uint32_t>(readlane(pmv, blk));
+    if (kProfile && pm == 0u) {                    // threshold above the counter width
+      ++ra.bk[0];
+      return;
+    }
     if (!ballot(((a.x | a.y | a.z | a.w) & pm) != 0)) {
       if (kProfile) ++ra.bk[1];
       return;
@@ -997,6 +1011,24 @@ __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __
     // (the offset wraps in 32 bits on purpose: base_j = lo_j - 4 pre_j may be
     // "negative", base_j + 4q is not)
     const uint32_t off = bj + 4u * static_cast<uint32_t>(q);
+#ifdef DPS_DEBUG
+    {
+      // a live lane's chunk lies inside its own venue's bucket [lo_j, hi_j) =
+      // [tile_off[b], tile_off[b+1]): its venue is the last lane j with
+      // pre_j <= q (pre is nondecreasing; lanes past the group hold pre = nq).
+      // Round 5's fault was this offset formed as pointer + a
+      // "negative" 32-bit base before the positive 4q was added.
+      int jt = -1;
+      for (int j = 0; j < kWave; ++j) jt += readlane(S.G.pre, j) <= q ? 1 : 0;
+      const int js = jt < 0 ? 0 : jt;
+      const uint32_t base_j = static_cast<uint32_t>(__shfl(static_cast<int>(S.G.base), js, kWave));
+      const int pre_j = __shfl(S.G.pre, js, kWave);
+      const int pre_n = js + 1 < kWave ? __shfl(S.G.pre, js + 1, kWave) : S.G.nq;
+      const uint32_t lo_j = base_j + 4u * static_cast<uint32_t>(pre_j);
+      const uint32_t len_j = 4u * static_cast<uint32_t>(pre_n - pre_j);
+      DPS_DASSERT(!live || (jt >= 0 && bj == base_j && off - lo_j < len_j));
+    }
+#endif
     const uint4* src = live ? reinterpret_cast<const uint4*>(ent + off) : kDeadChunk + lane;
     B.e[u] = *src;
     B.c[u] = live ? cj : 0;
@@ -1398,6 +1430,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
               if (last) { pc[5] += ts[5] - ts[2]; pc[6] += ts[6] - ts[5]; }
               ra.u8h += S_u8h ? 1u : 0u;            // passes over a u8 half tile
               ra.wide += S.lnp > 0 ? 1u : 0u;       // passes with wider counters
+              const int nq = S.G.nq;
+              const int hb = nq == 0 ? 0 : nq <= 16 ? 1 : nq <= 64 ? 2 : nq <= 128 ? 3
+                           : nq <= 192 ? 4 : nq <= 384 ? 5 : nq <= 768 ? 6 : 7;
+#pragma unroll
+              for (int i = 0; i < 8; ++i)
+                if (i == hb) {
+                  ++ra.nqh[i];
+                  ra.nqc[i] += static_cast<uint32_t>(nq);
+                  ra.nqe[i] += ts[4] - ts[3];
+                }
             }
             if (last) break;
           }
@@ -1462,6 +1504,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
     atomicAdd(p.counter + 18, static_cast<unsigned long long>(ra.wide));
 #pragma unroll
     for (int i = 0; i < 5; ++i) atomicAdd(p.counter + 19 + i, static_cast<unsigned long long>(ra.bk[i]));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      atomicAdd(p.counter + 24 + i, static_cast<unsigned long long>(ra.nqh[i]));
+      atomicAdd(p.counter + 32 + i, static_cast<unsigned long long>(ra.nqc[i]));
+      atomicAdd(p.counter + 40 + i, static_cast<unsigned long long>(ra.nqe[i]));
+    }
   }
 }
 

@@ -1516,8 +1516,13 @@ int dps_global_walks(const int64_t* c_ptr, const int32_t* c_col, const int32_t* 
   return DPS_OK;
 }
 
+// The bucketed column sums (more than kSumLds mids, at most kCsMaxRanges
+// ranges of kWideMids) hold one 8-byte (mid | author flag, C) pair per C entry:
+// 8 B x nnz_cap of HBM on top of the per-range counts; other shapes need none.
 size_t dps_walks_workspace_size(int64_t nnz_cap, int64_t n_mids) {
-  if (n_mids <= kSumLds || nnz_cap <= 0) return 256;
+  if (n_mids <= kSumLds || nnz_cap <= 0 ||
+      n_mids > static_cast<int64_t>(kCsMaxRanges) * kWideMids)
+    return 256;
   const int64_t nr = (n_mids + kWideMids - 1) / kWideMids;
   const int64_t m = nr * kCsBlocks;
   return align_up(static_cast<size_t>(m) * sizeof(uint32_t)) +
@@ -1540,8 +1545,9 @@ int dps_walks_fused_ws(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   DPS_REQUIRE(n_rows >= 0 && n_authors >= 0 && n_authors <= n_rows && n_mids >= 0,
               DPS_ERR_INVALID, "bad sizes");
   DPS_REQUIRE(c_ptr && g && (n_mids == 0 || (s && n_v)), DPS_ERR_INVALID, "null array");
-  DPS_REQUIRE(n_mids <= static_cast<int64_t>(kCsMaxRanges) * kWideMids || ws == nullptr,
-              DPS_ERR_INVALID, "too many mids for the bucketed column sums");
+  // more mids than the bucketed column sums cover (kCsMaxRanges ranges) take
+  // the range-by-range k_col_sums_wide below, as without a workspace
+  const bool bucketed = n_mids <= static_cast<int64_t>(kCsMaxRanges) * kWideMids;
   auto st = static_cast<hipStream_t>(stream);
   {
     FillSet fs;   // stats, s and n_v zeroed in one launch
@@ -1553,7 +1559,7 @@ int dps_walks_fused_ws(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     DPS_HIP_RET(fill_set(fs, st));
   }
   if (n_mids > 0) {
-    if (n_rows > 0 && n_mids > kSumLds && ws != nullptr && nnz_cap > 0) {
+    if (n_rows > 0 && n_mids > kSumLds && bucketed && ws != nullptr && nnz_cap > 0) {
       // bucketed by mid range (nnz_cap >= nnz C: the caller's bound, as for
       // the SpGEMM output; the scatter never writes past it)
       DPS_REQUIRE(ws_bytes >= dps_walks_workspace_size(nnz_cap, n_mids), DPS_ERR_WORKSPACE,

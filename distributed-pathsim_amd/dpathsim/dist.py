@@ -103,6 +103,36 @@ class RcclComm:
             pass
 
 
+def check_comm_gather(comm, device, group=None, n: int = 4099) -> bool:
+    """One gather of a known pattern through ``comm`` (anything with
+    ``rank``/``world``/``gather(send, recv, root)``, e.g. :class:`RcclComm`),
+    checked by rank 0 in this process; the verdict is shared over ``group``
+    (the control-plane group: gloo in bench.py) so every rank returns the same
+    answer.  A gather that raises counts as a mismatch.  bench.py runs it once
+    before its timed loop and, on a mismatch, takes the torch nccl group for
+    the top-k gather instead (VERDICT r05 #7)."""
+    device = torch.device(device)
+    ok = True
+    try:
+        ar = torch.arange(n, dtype=torch.int64, device=device)
+        send = ar * 1000003 + comm.rank * 7919 + 1
+        recv = (torch.full((comm.world * n,), -1, dtype=torch.int64, device=device)
+                if comm.rank == 0 else None)
+        comm.gather(send, recv, root=0)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        if comm.rank == 0:
+            want = torch.cat([ar * 1000003 + r * 7919 + 1 for r in range(comm.world)])
+            ok = bool(torch.equal(recv, want))
+    except Exception:       # noqa: BLE001 -- any failure means: do not use this path
+        ok = False
+    nccl = dist.get_backend(group) == "nccl"
+    verdict = torch.tensor([1 if ok else 0], dtype=torch.int64,
+                           device=device if nccl else "cpu")
+    dist.all_reduce(verdict, op=dist.ReduceOp.MIN, group=group)
+    return int(verdict.item()) == 1
+
+
 class TileSplit:
     """The N > 1 build's tile split (PathSimEngine.split): rank r builds the C^T
     tiles of its own target-tile range (dps_label_rows + dps_ct_tiles_build2

@@ -128,7 +128,6 @@ class PathSimEngine:
         # N > 1 (dist.TileSplit): this rank builds the C^T tiles of its own
         # target-tile range only and the ranks all-gather the slices
         self.split = None
-        self._split_state = {}
         self.info = BuildInfo()
         self.built = False
         self.checked = False
@@ -292,8 +291,9 @@ class PathSimEngine:
                       _ptr(t_rank), _ptr(g_t), _ptr(ows), ows.numel(), st)
             del ows
             mark("order")
-            split = self.split if self.split is not None and self.split.world > 1 else None
-            self._split_state = {}
+            # (no authors: nothing to split, every rank builds the empty tiles)
+            split = (self.split if self.split is not None and self.split.world > 1 and NA > 0
+                     else None)
             T = max(1, math.ceil(NA / self.tile_w)) if NA else 1
             ent_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV, NA,
                                 self.tile_w)
@@ -413,8 +413,10 @@ class PathSimEngine:
         """Tiles of width W over this rank's labels (dps_ct_tiles_build2 on the
         sub-C), packed into a slice (dps_tiles_pack), all-gathered, assembled
         into the full layout (dps_tiles_assemble).  The slice's entry capacity
-        is the plan in split.caps[W] (the largest slice of an earlier build of
-        the same graph, see check()) or, before one exists, the host bound."""
+        is the plan in split.caps under this graph's key (_plan_key): the
+        largest slice over the ranks, read back and max-reduced once, at the
+        first build of the graph (one host sync and one collective); later
+        builds of the same graph produce the same slices and reuse it."""
         l0, l1, sub_ptr, sub_col, sub_val = sub
         NA, NV = self.typed.n_authors, self.typed.n_mids
         st = self.stream
@@ -424,8 +426,7 @@ class PathSimEngine:
         T = max(1, math.ceil(NA / W)) if NA else 1
         n = l1 - l0
         tl = -(-n // W)
-        # (the host bound over the largest range, the same on every rank: the
-        # gathered slices must all have one size)
+        # (the host bound over the largest range: the local build's capacity)
         loc_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV,
                             tr_unit * self.tile_w, W)
         loc_off = self._empty(NV * tl + 1, torch.int32)
@@ -440,7 +441,13 @@ class PathSimEngine:
                       None, n, NV, W, bnd.expand, _ptr(loc_off), _ptr(loc_ent), _ptr(loc_maxc),
                       _ptr(loc_gmin), _ptr(status), _ptr(ws), ws.numel(), st)
             del ws
-        cap = int(split.caps.get(W, loc_cap))
+        key = self._plan_key(split, W)
+        if key not in split.caps:
+            # the gathered slices must all have one size: the largest real slice
+            # (not world x the whole graph's bound)
+            words = int(loc_off[NV * tl].item()) if tl else 0
+            split.caps[key] = (split.allreduce_max(words) + 3) // 4 * 4
+        cap = int(split.caps[key])
         words = _lib.size("dps_tiles_slice_words", NV, tr, cap)
         sl = self._empty(words, torch.int32)
         _lib.call("dps_tiles_pack", _ptr(loc_off), _ptr(loc_maxc), _ptr(loc_gmin), _ptr(loc_ent),
@@ -455,18 +462,15 @@ class PathSimEngine:
         _lib.call("dps_tiles_assemble", _ptr(gathered), split.world, NV, T, tr, cap, _ptr(off),
                   _ptr(ent), ent.numel(), _ptr(maxc), _ptr(gm), _ptr(status), _ptr(ws), ws.numel(),
                   st)
-        # the slice's entry words, for the plan (read by check())
-        self._split_state[W] = loc_off[NV * tl: NV * tl + 1] if tl else None
         return off, ent, maxc, gm, status
 
-    def _split_plan(self):
-        """After a split build (collective: every rank calls it): the largest
-        slice over the ranks per tile width becomes the gather capacity of the
-        next builds."""
-        split = self.split
-        for W, t in self._split_state.items():
-            words = int(t.item()) if t is not None else 0
-            split.caps[W] = (split.allreduce_max(words) + 3) // 4 * 4
+    def _plan_key(self, split, W):
+        """The split plan's key: the tile width and the graph's shape and host
+        bounds (a TileSplit reused for another graph or other bounds
+        must not gather with the old graph's capacity)."""
+        bnd = self.bounds
+        return (int(W), self.typed.n_authors, self.typed.n_mids, int(bnd.expand), int(bnd.sum_c),
+                split.world, self.tile_w)
 
     def check(self):
         """Read the build's statistics back (one synchronisation) and raise if a
@@ -493,9 +497,6 @@ class PathSimEngine:
         if status_h == DPS_ERR_OVERFLOW and self.split is not None and self.split.world > 1 \
                 and self.info.max_c <= 0xFFFF:
             raise RuntimeError("a tile slice outgrew the gather capacity of the split build's plan")
-        if self.split is not None and self.split.world > 1 and self._split_state and \
-                not all(W in self.split.caps for W in self._split_state):
-            self._split_plan()
         if info.expand > self.bounds.sum_c:   # impossible by construction (raw >= distinct)
             raise RuntimeError(f"nnz(C) {info.expand} exceeds its bound {self.bounds.sum_c}")
         if status_h != 0 or info.max_c > 0xFFFF:

@@ -239,7 +239,10 @@ int dps_walks_fused(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c
 /* The same with a workspace (dps_walks_workspace_size(nnz_cap, n_mids) bytes,
  * 256-byte aligned; nnz_cap >= nnz C, e.g. the SpGEMM output capacity): with
  * more mids than one LDS range the column sums bucket C's entries by mid range
- * once instead of re-reading C per range.  ws == NULL: as dps_walks_fused. */
+ * once instead of re-reading C per range.  ws == NULL: as dps_walks_fused.
+ * Memory: the bucketed path holds one 8-byte pair per C entry (8 B x nnz_cap)
+ * plus per-range counts; with at most 6144 mids, or more than 4096 x 12288,
+ * the workspace is 256 bytes and the call takes the unbucketed path. */
 size_t dps_walks_workspace_size(int64_t nnz_cap, int64_t n_mids);
 int dps_walks_fused_ws(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
                        int64_t n_rows, int64_t n_authors, int64_t n_mids, int64_t* s,

@@ -475,3 +475,50 @@ def test_read_topk_shards_rejects_stale_or_mixed(tmp_path):
     m0.write_text(json.dumps(dict(meta0, row_begin=1)))
     with pytest.raises(ValueError, match="row 0"):
         read_topk_shards(str(tmp_path))
+
+
+class _GlooComm:
+    """A stand-in for dist.RcclComm over the gloo group (CPU tensors): a true
+    gather, a corrupting one, or one that raises."""
+
+    def __init__(self, mode):
+        self.rank, self.world, self.mode = dist.get_rank(), dist.get_world_size(), mode
+
+    def gather(self, send, recv, root=0):
+        parts = [torch.empty_like(send) for _ in range(self.world)] if self.rank == root else None
+        dist.gather(send, gather_list=parts, dst=root)
+        if self.mode == "raise" and self.rank == 1:      # an error status after the call
+            raise RuntimeError("simulated dps_gather failure")
+        if self.rank == root:
+            recv.copy_(torch.cat(parts))
+            if self.mode == "corrupt":
+                recv[-1] += 1
+
+
+def _comm_check_worker(rank, world, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dpathsim.dist import check_comm_gather
+        got = [check_comm_gather(_GlooComm(m), "cpu") for m in ("good", "corrupt", "raise")]
+        if rank == 0:
+            with open(result_path, "w") as f:
+                f.write(",".join(str(g) for g in got))
+        else:
+            with open(f"{result_path}.{rank}", "w") as f:
+                f.write(",".join(str(g) for g in got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_check_comm_gather_verdict_on_every_rank(tmp_path, world):
+    """bench.py's pre-timing check of the C-ABI gather: a true
+    gather passes, a corrupted or failing one fails -- and every rank gets the
+    same verdict, so all of them take the same gather path."""
+    out = tmp_path / "result.txt"
+    mp.start_processes(_comm_check_worker, args=(world, _free_port(), str(out)), nprocs=world,
+                       join=True, start_method="spawn")
+    assert out.read_text() == "True,False,False"
+    for r in range(1, world):
+        assert (tmp_path / f"result.txt.{r}").read_text() == "True,False,False"

@@ -17,13 +17,15 @@ pytestmark = pytest.mark.gpu
 class _Recorder:
     """A TileSplit stand-in for rank r of `world`: its all-gather keeps the
     slice it is sent (calls in build order) and hands back `slices` where
-    provided."""
+    provided; its max over ranks records the values it is sent and returns
+    `maxima` (in call order) where provided."""
 
-    def __init__(self, rank, world, slices=None, caps=None):
+    def __init__(self, rank, world, slices=None, maxima=None):
         self.rank, self.world = rank, world
         self.sent, self.slices = [], slices
-        self.caps = dict(caps or {})
+        self.caps = {}
         self.calls = 0
+        self.seen, self.maxima = [], maxima
 
     def allgather(self, send, recv):
         self.sent.append(send.clone())
@@ -34,7 +36,8 @@ class _Recorder:
         self.calls += 1
 
     def allreduce_max(self, v):
-        return int(v)
+        self.seen.append(int(v))
+        return int(self.maxima[len(self.seen) - 1]) if self.maxima else int(v)
 
 
 def _bucket_multisets_equal(off_a, ent_a, off_b, ent_b, w):
@@ -54,20 +57,32 @@ def _bucket_multisets_equal(off_a, ent_a, off_b, ent_b, w):
     return len(a) == len(b) and np.array_equal(a[np.lexsort((a, ba))], b[np.lexsort((b, bb))])
 
 
-def _split_engine(t, world, tile_w=None):
-    """Build every rank's slices (recording them), then rank 0's engine with
-    the gathered slices (the first build of a graph: host-bound capacities)."""
-    from dpathsim.engine import PathSimEngine
-    recs = []
+def _record(t, world, tile_w, maxima):
+    out = []
     for r in range(world):
-        e = PathSimEngine(t, tile_w=tile_w)
-        e.split = _Recorder(r, world)
+        e = PathSimEngine_(t, tile_w=tile_w)
+        e.split = _Recorder(r, world, maxima=maxima)
         e.upload().build(check=False)
         torch.cuda.synchronize()
-        recs.append(e.split.sent)
+        out.append(e.split)
         del e
-    eng = PathSimEngine(t, tile_w=tile_w)
-    eng.split = _Recorder(0, world, slices=recs)
+    return out
+
+
+def PathSimEngine_(*a, **kw):
+    from dpathsim.engine import PathSimEngine
+    return PathSimEngine(*a, **kw)
+
+
+def _split_engine(t, world, tile_w=None):
+    """Every rank's first build: the plan (each rank's real slice size, one
+    max per tile width); then every rank's slices at the plan's capacity
+    (recorded), and rank 0's engine with the gathered slices."""
+    seen = [s.seen for s in _record(t, world, tile_w, None)]
+    maxima = [max(v[i] for v in seen) for i in range(len(seen[0]))]
+    recs = [s.sent for s in _record(t, world, tile_w, maxima)]
+    eng = PathSimEngine_(t, tile_w=tile_w)
+    eng.split = _Recorder(0, world, slices=recs, maxima=maxima)
     eng.upload().build()
     return eng
 
@@ -122,10 +137,42 @@ def test_split_slice_overflow_is_reported():
     recs = []
     for r in range(2):
         e = PathSimEngine(t)
-        e.split = _Recorder(r, 2, caps={16384: 64, 8192: 64})
+        e.split = _Recorder(r, 2, maxima=[64, 64])
         e.upload().build(check=False)
         recs.append(e.split.sent)
     eng = PathSimEngine(t)
-    eng.split = _Recorder(0, 2, slices=recs, caps={16384: 64, 8192: 64})
+    eng.split = _Recorder(0, 2, slices=recs, maxima=[64, 64])
     with pytest.raises(RuntimeError, match="gather capacity"):
         eng.upload().build()
+
+
+def test_split_plan_is_per_graph():
+    """one TileSplit reused for a second, larger graph must not
+    gather with the first graph's capacity (the plan is keyed by the graph);
+    the second graph's assembled tiles still give the oracle's top-k."""
+    import pathsim_oracle as po
+    from dpathsim.synth import synth_config
+    small = synth_config("config3", scale=0.01).typed()
+    big = synth_config("config3", scale=0.05).typed()
+    # world 2, one split object for both graphs: two plans, the slices of
+    # each graph at its own capacity
+    maxima_small = [max(v[i] for v in (s.seen for s in _record(small, 2, None, None)))
+                    for i in range(2)]
+    maxima_big = [max(v[i] for v in (s.seen for s in _record(big, 2, None, None)))
+                  for i in range(2)]
+    assert maxima_big[0] > maxima_small[0]
+    recs_small = [s.sent for s in _record(small, 2, None, maxima_small)]
+    recs_big = [s.sent for s in _record(big, 2, None, maxima_big)]
+    shared = _Recorder(0, 2, slices=recs_small, maxima=maxima_small + maxima_big)
+    e1 = PathSimEngine_(small)
+    e1.split = shared
+    e1.upload().build()
+    shared.slices, shared.calls = recs_big, 0
+    e2 = PathSimEngine_(big)
+    e2.split = shared
+    e2.upload().build()
+    assert len(shared.caps) == 4 and len(shared.seen) == 4
+    want = po.COracle.from_typed(big).topk(10, 0, big.n_authors)
+    got = [a.cpu().numpy() for a in e2.topk(10)]
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+    assert np.array_equal(got[2].view(np.int64), want[2].view(np.int64))

@@ -30,8 +30,8 @@ for W, NW in cases:
         if os.environ.get("AB_NHEAVY"):
             eng.n_heavy = int(os.environ["AB_NHEAVY"])
         # optimistic 4-bit passes (engine.opt_passes, dps_cct_ext.tile_sum): on in
-        # A/B runs unless AB_OPT=0 (a library without them ignores tile_sum)
-        eng.opt_passes = os.environ.get("AB_OPT", "1") == "1"
+        # A/B runs only with AB_OPT=1 (the engine default is off)
+        eng.opt_passes = os.environ.get("AB_OPT", "0") == "1"
         if os.environ.get("AB_SPLIT"):      # "rows:pieces" of the heavy-row split
             eng.split_rows, eng.pieces = (int(v) for v in os.environ["AB_SPLIT"].split(":"))
         eng.upload().build()

@@ -15,7 +15,7 @@ for ab in ("0", "16"):
     e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
     e0.record(); eng.topk(10, 0, R); e1.record(); torch.cuda.synchronize()
     print(f"ablate {ab}: {e0.elapsed_time(e1):.2f} ms", flush=True)
-c = eng.tensor("topk_ws")[:256].view(torch.int64).cpu().tolist()
+c = eng.tensor("topk_ws")[:512].view(torch.int64).cpu().tolist()
 st = max(c[12], 1)
 names = ["scatter", "flush+thresholds", "prefetch", "epilogue"]
 tot = sum(c[8:12])
@@ -30,3 +30,11 @@ nb = max(sum(c[19:23]), 1)
 print(f"epilogue blocks {nb} ({nb / st:.2f} per stage): above counter width {c[19] / nb:.1%}, "
       f"prefilter empty {c[20] / nb:.1%}, exact empty {c[21] / nb:.1%}, with candidates {c[22] / nb:.1%}; "
       f"extraction rounds {c[23]} ({c[23] / max(c[22], 1):.2f} per candidate block)", flush=True)
+edges = ["0", "1-16", "17-64", "65-128", "129-192", "193-384", "385-768", ">768"]
+npass = max(sum(c[24:32]), 1)
+epi = max(sum(c[40:48]), 1)
+print("passes by the stage's chunk count (share of passes / of chunks / of epilogue cycles, "
+      "epilogue cycles per pass):", flush=True)
+for i, e in enumerate(edges):
+    print(f"  {e:>8}: {c[24 + i] / npass:6.1%} {c[32 + i] / max(sum(c[32:40]), 1):6.1%} "
+          f"{c[40 + i] / epi:6.1%}  {c[40 + i] / max(c[24 + i], 1):7.0f}", flush=True)

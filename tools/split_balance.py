@@ -35,10 +35,11 @@ NA = t.n_authors
 
 
 class Split:
-    def __init__(self, rank, world, slices=None, caps=None):
+    def __init__(self, rank, world, slices=None, maxima=None):
         self.rank, self.world, self.slices = rank, world, slices
-        self.caps = dict(caps or {})
+        self.caps = {}                  # the engine's plan, keyed by graph and width
         self.sent, self.calls, self.bytes = [], 0, 0
+        self.seen, self.maxima = [], maxima
 
     def allgather(self, send, recv):
         if self.slices is None:
@@ -50,8 +51,9 @@ class Split:
             self.bytes += src.numel() * src.element_size()
         self.calls += 1
 
-    def allreduce_max(self, v):
-        return int(v)
+    def allreduce_max(self, v):      # the plan: every rank's real slice size
+        self.seen.append(int(v))
+        return int(self.maxima[len(self.seen) - 1]) if self.maxima else int(v)
 
 
 def ev_time(fn, reps=3):
@@ -86,14 +88,13 @@ for world in (2, 4, 8):
         e.split = Split(r, world)
         e.upload().build(check=False)
         torch.cuda.synchronize()
-        sent.append((e.split.sent, {W: (int(v.item()) if v is not None else 0)
-                                    for W, v in e._split_state.items()}))
+        sent.append((e.split.sent, e.split.seen))
         del e
-    caps = {W: (max(s[1][W] for s in sent) + 3) // 4 * 4 for W in sent[0][1]}
+    maxima = [max(s[1][i] for s in sent) for i in range(len(sent[0][1]))]
     sent = []
     for r in range(world):
         e = PathSimEngine(t)
-        e.split = Split(r, world, caps=caps)
+        e.split = Split(r, world, maxima=maxima)
         e.upload().build(check=False)
         torch.cuda.synchronize()
         sent.append(e.split.sent)
@@ -105,7 +106,7 @@ for world in (2, 4, 8):
     rows = []
     for r in range(world):
         e = PathSimEngine(t)
-        e.split = Split(r, world, slices=gathered, caps=caps)
+        e.split = Split(r, world, slices=gathered, maxima=maxima)
         e.upload()
 
         def step(e=e):
