@@ -182,20 +182,20 @@ def test_c_abi_rejects_bad_arguments_without_gpu():
     assert rc == _lib.DPS_ERR_UNSUPPORTED     # k = 0
     assert lib.dps_csr_build_workspace_size(100, 10) > 0
     # venue skipping: the struct's table width and pointers are validated too
-    ws = C.create_string_buffer(512)
+    ws = C.create_string_buffer(1024)
     ws_al = (C.addressof(ws) + 255) // 256 * 256
     vs = _lib.CctExt(1, 1, 1, 65, None, None, None, None)
     rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 256, 8, 8, None, 8,
-                          C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 256, None)
+                          C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 512, None)
     assert rc == _lib.DPS_ERR_INVALID and b"n_hv" in lib.dps_last_error()
     vs = _lib.CctExt(1, None, 1, 32, None, None, None, None)
     rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 256, 8, 8, None, 8,
-                          C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 256, None)
+                          C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 512, None)
     assert rc == _lib.DPS_ERR_INVALID and b"venue skipping" in lib.dps_last_error()
     # companion u8 tiles belong to tile_w 16384 only
     vs = _lib.CctExt(None, None, None, 0, 8, 8, 8, None)
     rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 256, 8, 8, None, 8,
-                          C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 256, None)
+                          C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 512, None)
     assert rc == _lib.DPS_ERR_INVALID and b"16384" in lib.dps_last_error()
     assert lib.dps_heavy_venues(None, 10, 0, None, None) == _lib.DPS_ERR_INVALID
     assert lib.dps_heavy_table(None, None, None, None, 10, None, 65, None, None) == _lib.DPS_ERR_INVALID
