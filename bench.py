@@ -246,7 +246,8 @@ def main():
     n_pass, n_chunk, n_ver = kc["passes"], kc["chunks"], kc["verified"]
     bytes_launch = ent_bytes * terms + 20 * shard * k + 8 * (shard + 1)
     hbm_achieved = bytes_launch / (topk_ms * 1e-3) / 1e9
-    ctr_bytes = 0.5 if args.tile_w == 16384 else 1.0 if args.tile_w <= 8192 else 4.0
+    ctr_bytes = 0.5 if args.tile_w in (16384, 15360) else 1.0 if args.tile_w <= 8192 else 4.0
+    acc_bytes = 7680 if args.tile_w in (7680, 15360) else 8192   # one pass's accumulator
     pairs_launch = shard * (NA - 1)
     lds_rate = {"scatter_add_b32": LDS_ADD_B32, "acc_read_b128": LDS_READ_B128,
                 "acc_zero_b128": LDS_WRITE_B128}
@@ -263,8 +264,8 @@ def main():
     lds_achieved = lds_equiv / (topk_ms * 1e-3) / 1e9
     # executed: what the kernel counted (k_cct1 only: 16-byte chunks scattered, 8 KiB
     # accumulator passes read and zeroed)
-    exe_cls = {"scatter_add_b32": 32 * n_chunk, "acc_read_b128": 8192 * n_pass,
-               "acc_zero_b128": 8192 * n_pass}
+    exe_cls = {"scatter_add_b32": 32 * n_chunk, "acc_read_b128": acc_bytes * n_pass,
+               "acc_zero_b128": acc_bytes * n_pass}
     exe_floor_ms, _ = lds_price(exe_cls)
     traffic, pmc = None, {}
     if args.pmc_json and os.path.exists(args.pmc_json):

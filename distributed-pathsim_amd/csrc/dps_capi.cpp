@@ -26,6 +26,9 @@ int dps_set_tuning(int32_t key, int32_t value) {
   if (key == DPS_TUNE_BANK_ORDER)
     DPS_REQUIRE(value >= 0 && value <= 2, DPS_ERR_INVALID,
                 "bank order must be 0 (automatic), 1 (on) or 2 (off), got %d", value);
+  if (key == DPS_TUNE_LEAN_WPC)
+    DPS_REQUIRE(value >= 0 && value <= 32, DPS_ERR_INVALID,
+                "workgroups per CU must be 0 (automatic) or 1..32, got %d", value);
   dps::g_tune[key].store(value);
   return DPS_OK;
 }

@@ -352,10 +352,13 @@ __global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(4)))
       for (int64_t yb = 0; slot < want && yb < p.n_targets; yb += kWave) {
         const int64_t yc = yb + lane;
         bool ok = yc < p.n_targets && yc != x;
+#pragma unroll
         for (int q = 0; q < KPL; ++q) {
           for (int l = 0; l < kWave; ++l) {
             if (q * kWave + l >= top.filled) break;
-            ok = ok && (readlane(top.y[q], l) != static_cast<int>(yc));
+            // (a plain AND, not &&: see the same loop in dps_cct1.hip)
+            const int yl = readlane(top.y[q], l);
+            ok = ok & (yl != static_cast<int>(yc));
           }
         }
         const uint64_t mk = ballot(ok);
@@ -698,7 +701,9 @@ using namespace dps;
 
 extern "C" {
 
-size_t dps_cct_topk_workspace_size(void) { return 512; }
+// 64 counters; the profiling build adds four words per wave of the lean
+// kernel (start, end, start of its last row, that row) for tools/wave_times.py
+size_t dps_cct_topk_workspace_size(void) { return kProfile ? 512 + 32 * 16384 : 512; }
 
 size_t dps_heavy_first_workspace_size(int64_t n_rows) {
   const size_t m = static_cast<size_t>(n_rows > 0 ? n_rows : 1);
@@ -764,9 +769,10 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
                          const int32_t* piece_t0 = nullptr, const int32_t* piece_t1 = nullptr,
                          int32_t* piece_idx = nullptr, int64_t* piece_cnt = nullptr,
                          double* piece_score = nullptr, const SymSetup* sy = nullptr) {
-  const int shift = log2_exact(tile_w);
+  const TileDim td = tile_dim(tile_w);
+  const int shift = td.shift;
   DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED,
-              "tile_w must be a power of two in [256, 65536], got %d", tile_w);
+              "tile_w must be a power of two in [256, 65536], 7680 or 15360, got %d", tile_w);
   DPS_REQUIRE(k >= 1 && k <= 256, DPS_ERR_UNSUPPORTED, "k must be in [1, 256], got %d", k);
   DPS_REQUIRE(n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "n_targets exceeds int32");
   DPS_REQUIRE(n_mids * ((n_targets + tile_w - 1) / tile_w) < int64_t(UINT32_MAX), DPS_ERR_OVERFLOW,
@@ -785,7 +791,7 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   }
   const bool half = ext && ext->half_ent;
   if (half) {
-    DPS_REQUIRE(shift == 14, DPS_ERR_INVALID, "companion u8 tiles need tile_w 16384");
+    DPS_REQUIRE(shift == 14, DPS_ERR_INVALID, "companion u8 tiles need tile_w 16384 or 15360");
     DPS_REQUIRE(ext->half_off && (ext->half_maxc || !tile_maxc), DPS_ERR_INVALID,
                 "dps_cct_ext companion tiles need half_off (and half_maxc with tile_maxc)");
   }
@@ -799,7 +805,7 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   p.h_off = half ? ext->half_off : nullptr;
   p.h_ent = half ? ext->half_ent : nullptr;
   p.h_maxc = half ? (tile_maxc ? ext->half_maxc : ext->half_off) : nullptr;
-  p.T8 = (n_targets + 8191) / 8192;
+  p.T8 = (n_targets + tile_w / 2 - 1) / (tile_w / 2);   // companion half tiles
   p.tile_sum = half ? ext->tile_sum : nullptr;
   p.c_ptr = c_ptr; p.c_col = c_col; p.c_val = c_val;
   p.g = g; p.g_t = g_t ? g_t : g; p.t_perm = t_perm; p.t_rank = t_rank;
@@ -809,6 +815,7 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   p.n_targets = n_targets;
   p.T = (n_targets + tile_w - 1) / tile_w;
   p.shift = shift;
+  p.tile_w = tile_w;
   // waves per row: one wave owns a row for W <= 8192 (8 KB of u8 accumulators,
   // no barriers, one exact running top-k per row); wider tiles share a row
   // between the waves of a workgroup (4 x 32 KB or 2 x 64 KB per CU)
@@ -822,6 +829,9 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
   DPS_REQUIRE(nw != 8 || shift > 14, DPS_ERR_INVALID, "8 waves per row need tile_w >= 32768");
   DPS_REQUIRE(nw == 1 || shift != 14, DPS_ERR_UNSUPPORTED,
               "tile_w 16384 (4-bit counter entries) runs one wave per row");
+  DPS_REQUIRE(!td.t15 || (nw == 1 && !sy && !(half && ext->tile_sum)), DPS_ERR_UNSUPPORTED,
+              "tile_w %d runs the one-wave kernel without the symmetric mode or the "
+              "optimistic passes", tile_w);
 
   p.dbuf = nw > 1 && shift <= 14;   // 2 x W bytes of u8 accumulators up to W = 16384, one 32 KB buffer above
   p.row_begin = row_begin; p.row_order = row_order; p.out_by_slot = out_by_slot;
@@ -859,14 +869,15 @@ static int cct_topk_impl(const int64_t* c_ptr, const int32_t* c_col, const int32
     if (const char* ab = std::getenv("DPATHSIM_ABLATE")) p.ablate = std::atoi(ab);
   // word 0: row dequeue counter; words 1-3: the lean kernel's pass / chunk /
   // table-completed candidate counts, word 4 its overflowed optimistic passes
-  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (p.ablate & 24) ? 512 : 8 * sizeof(unsigned long long), st));
+  // (the debug build also zeroes its check record, words 48..55)
+  DPS_HIP_RET(hipMemsetAsync(p.counter, 0, (kDebug || (p.ablate & 24)) ? 512 : 8 * sizeof(unsigned long long), st));
   // the bench shape (W = 8192, one wave per row) runs the lean kernel
   // (dps_cct1.hip); DPATHSIM_LEAN=0 selects this file's general kernel
   bool lean = (shift == 13 || shift == 14) && nw == 1 && (p.ablate == 0 || p.ablate == 16);
 #ifdef DPS_PROFILE
   if (const char* e = std::getenv("DPATHSIM_LEAN")) lean = lean && std::atoi(e) != 0;   // experiments
 #endif
-  if (lean || shift == 14) return cct1_launch(p, st);
+  if (lean || shift == 14 || td.t15) return cct1_launch(p, st);
   if (shift <= 13) return dispatch<true>(p, nw, k, st);   // 16-bit tile entries
   return dispatch<false>(p, nw, k, st);
 }

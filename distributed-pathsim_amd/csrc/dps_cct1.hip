@@ -92,6 +92,34 @@ template <> struct Fmt<2> {
   static constexpr int BITS = 4;
   static constexpr uint32_t UB0 = 0xFu;
 };
+// Tile geometry (round 6).  One-wave workgroups with 8 KiB of LDS run 18 per
+// CU, not 20: the LDS a CU gives its workgroups is ~150 KiB in 512-byte
+// granules (tools/ubench/resident.hip: 18 resident at 7712..8192 bytes, 20 at
+// 7680; the hot launch's wave stamps showed 512 of its 5120 workgroups
+// starting only at the end, tools/wave_times.py), so the T15 layout cuts a
+// tile to 15 / 16 of the power-of-two width -- 15360 targets in 4-bit
+// counters, 7680 in u8, 7680 bytes either way -- and 20 waves fit a CU.  A
+// tile's eight threshold segments (= epilogue trips) are then 960 bytes, read
+// by lanes 0..59 (lanes 60..63 re-read lane 59's bytes and are masked off).
+template <int F, bool T15>
+struct Geo {
+  static constexpr int W = (T15 ? 15 : 16) * (F == 1 ? 512 : 1024);   // targets per tile
+  static constexpr int TPD = F == 1 ? 4 : 8;          // targets per accumulator dword
+  static constexpr int SEGW = W / 8;                  // targets per segment (= per trip)
+  static constexpr int TRIP_DW = SEGW / TPD;          // dwords per trip: 256 or 240
+  static constexpr int LANES = TRIP_DW / 4;           // lanes reading 16 B of a trip
+  static constexpr int ACC_DW = 8 * TRIP_DW;          // accumulator dwords: 2048 or 1920
+};
+// Lane l's first dword within a trip (lanes past the trip's reuse the last one).
+template <int F, bool T15>
+__device__ __forceinline__ int trip_lane(int lane) {
+  return (Geo<F, T15>::LANES < kWave && lane >= Geo<F, T15>::LANES ? Geo<F, T15>::LANES - 1 : lane) * 4;
+}
+template <int F, bool T15>
+__device__ __forceinline__ uint32_t trip_mask(int lane) {
+  return Geo<F, T15>::LANES < kWave && lane >= Geo<F, T15>::LANES ? 0u : ~0u;
+}
+
 // Knobs, swept on the full config3 launch at W = 16384 (profiles/r03/ab7-ab9):
 // epilogue blocks per trip 1 / 2 = 72.3 / 73.2 ms; boundary selects before the
 // counting path 4 / 8 / 16 = 72.3 / 73.2 / 73.8 ms; flush the candidate queue
@@ -133,10 +161,12 @@ __device__ __forceinline__ uint32_t opt_check(const uint32_t* acc, uint32_t exp,
 // Zero the kEpi1 KiB of accumulator an epilogue trip has just read (dwords
 // b0..).  (ds_write_addtid_b32 zeroes 1.46x faster in isolation,
 // tools/ubench/addtid.hip, but did not move the kernel: DESIGN.md §6.)
+template <int F, bool T15>
 __device__ __forceinline__ void zero_trip(uint32_t* acc, int b0, int lane) {
 #pragma unroll
   for (int i = 0; i < kEpi1; ++i)
-    *reinterpret_cast<uint4*>(acc + b0 + i * kWave * 4 + lane * 4) = make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(acc + b0 + i * Geo<F, T15>::TRIP_DW + trip_lane<F, T15>(lane)) =
+        make_uint4(0, 0, 0, 0);
 }
 
 
@@ -304,7 +334,7 @@ struct Pend1 {
 constexpr uint32_t kOptMax = DPS_OPT_MAX;   // 0 = off
 constexpr uint32_t kOptSumMax = 0xFFFFu;    // bucket sums above this: no opt pass
 
-template <int F, bool HV, bool SY>
+template <int F, bool HV, bool SY, bool T15>
 __device__ __forceinline__ void pend_load(const CctParams& p, Pend1& P, int t, uint32_t ub, bool u8h,
                                           int d0, uint32_t vT, uint32_t vT8, int lane, int far,
                                           bool opt = false, uint32_t hb = 0) {
@@ -333,8 +363,9 @@ __device__ __forceinline__ void pend_load(const CctParams& p, Pend1& P, int t, u
     }
   }
   if (lane < 8) {
-    const int sh = u8h ? Fmt<1>::S : Fmt<F>::S, sg = u8h ? Fmt<1>::SEG : Fmt<F>::SEG;
-    const int64_t i = (static_cast<int64_t>(t) << sh) + (static_cast<int64_t>(lane) << sg);
+    const int64_t w = u8h ? Geo<1, T15>::W : Geo<F, T15>::W;
+    const int64_t sw = u8h ? Geo<1, T15>::SEGW : Geo<F, T15>::SEGW;
+    const int64_t i = static_cast<int64_t>(t) * w + static_cast<int64_t>(lane) * sw;
     P.gs = p.g_t[i < p.n_targets ? i : p.n_targets - 1];
     if (SY && (u8h ? (t >> 1) : t) >= far) P.tb = ld_fresh(p.tau_blk + ((i < p.n_targets ? i : p.n_targets - 1) >> 11));
   }
@@ -618,25 +649,28 @@ __device__ __forceinline__ void vq_flush(const CctParams& p, VQ& Q, TopK<KPL>& t
 // u16 / u32 pass epilogue (UB > 255, rare): scan + zero the accumulator of
 // pass `pass` (2 or 1 targets per dword), queue targets reaching their
 // segment's threshold.
-template <int F, int KPL, bool HV, bool SY>
+template <int F, int KPL, bool HV, bool SY, bool T15>
 __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                           const Stage& S, int lane, int64_t x_lab, int64_t gx,
                                           int mseg, int c, uint32_t hv, uint64_t hm, RowAux& ra) {
-  constexpr int kS1 = Fmt<F>::S, kSeg1 = Fmt<F>::SEG;
+  using G = Geo<F, T15>;
   const int lnp = S.lnp;
   const int bits = Fmt<F>::BITS << lnp;              // 8..32
   const int tpd_shift = (F == 1 ? 2 : 3) - lnp;      // log2(targets per dword)
   const uint32_t vmask = bits == 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
   const int blnp = bits == 8 ? 0 : bits == 16 ? 1 : 2;   // block_any's counter width
-  const int64_t tile_base = static_cast<int64_t>(S.t) << kS1;
-  const int pass_base = S.pass << (kS1 - lnp);
-  for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4) {
+  const int64_t tile_base = static_cast<int64_t>(S.t) * G::W;
+  const int pass_base = S.pass * (G::W >> lnp);
+  // (T15: the 1920-dword accumulator in 1 KiB rows, the last one half used)
+  for (int b0 = 0; b0 < G::ACC_DW; b0 += kWave * 4) {
     const int b = b0 + lane * 4;
-    const uint4 a = *reinterpret_cast<const uint4*>(acc + b);
-    *reinterpret_cast<uint4*>(acc + b) = make_uint4(0, 0, 0, 0);
+    const bool in = !T15 || b < G::ACC_DW;
+    const uint4 a = in ? *reinterpret_cast<const uint4*>(acc + b) : make_uint4(0, 0, 0, 0);
+    if (in) *reinterpret_cast<uint4*>(acc + b) = make_uint4(0, 0, 0, 0);
     const int i0 = pass_base + (b << tpd_shift);     // first target of this lane's 16 bytes
-    const uint32_t m = static_cast<uint32_t>(__shfl(mseg, (i0 >> kSeg1) & (kWave - 1), kWave));
-    const bool any = block_any(a, m, blnp);
+    const int sg = i0 / G::SEGW;                     // its threshold segment
+    const uint32_t m = static_cast<uint32_t>(__shfl(mseg, sg & (kWave - 1), kWave));
+    const bool any = in && block_any(a, m, blnp);
     if (!ballot(any)) continue;
 #pragma unroll 1
     for (int v = 0; v < (128 / bits); ++v) {
@@ -656,16 +690,18 @@ __device__ __forceinline__ void epi1_wide(const CctParams& p, uint32_t* acc, Top
 // 4-bit epilogue over the whole W = 16384 tile: 8 blocks of 2048 targets (one
 // threshold segment each; lane l reads dwords 4l..4l+3 of the block = targets
 // 32l..32l+31), read and zeroed kEpi1 at a time; candidates queued as in epi1_u8.
-template <int KPL, bool HV, bool SY>
+// T15: W = 15360, 8 trips of 1920 targets over lanes 0..59.
+template <int KPL, bool HV, bool SY, bool T15>
 __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                         int t, int lane, int x_lab, int64_t gx, int mseg,
                                         int c, uint32_t hv, uint64_t hm, RowAux& ra,
                                         uint32_t bmask, uint32_t oexp, uint32_t& bad) {
-  constexpr int kS = Fmt<2>::S, kSeg = Fmt<2>::SEG;
-  const int tile_base = t << kS;                         // labels < 2^31
+  using G = Geo<2, T15>;
+  const int tile_base = t * G::W;                        // labels < 2^31
   const int xr = x_lab - tile_base;
-  const bool xin = static_cast<uint32_t>(xr) < (1u << kS);   // the source is a target of this tile
+  const bool xin = static_cast<uint32_t>(xr) < static_cast<uint32_t>(G::W);   // the source is a target here
   const int xrel = xin ? xr : 0;
+  const uint32_t lmask = trip_mask<2, T15>(lane);        // (all ones unless T15)
   // optimistic pass judged here (oexp != 0, DPS_OPT_INEPI): each half's
   // candidates are held in the queue (no flush) until its digit sum shows no
   // overflowed count; a bad half's candidates are dropped (Q.n back to snap)
@@ -678,7 +714,7 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
   const uint32_t pmv = mu > 15u ? 0u : (0x10u - (0x80000000u >> __builtin_clz(mu | 1u))) * 0x11111111u;
   auto block = [&](uint4 a, int blk) {
     if (!((bmask >> blk) & 1u)) return;            // overflowed half (optimistic pass)
-    const uint32_t pm = static_cast<uint32_t>(readlane(pmv, blk));
+    const uint32_t pm = static_cast<uint32_t>(readlane(pmv, blk)) & lmask;
     if (kProfile && pm == 0u) {                    // threshold above the counter width
       ++ra.bk[0];
       return;
@@ -702,8 +738,9 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
       auto ge = [K](uint32_t v) { return (v & ((v & 0x77777777u) + K)) & 0x88888888u; };
       F4 = ge(a.x) | (ge(a.y) >> 1) | (ge(a.z) >> 2) | (ge(a.w) >> 3);
     }
+    F4 &= lmask;
 
-    const int i0 = (blk << kSeg) + (lane << 5);
+    const int i0 = blk * G::SEGW + (lane << 5);
     if (__builtin_expect(xin, false)) {            // the source itself never counts
       const int rel = xrel - i0;
       if (rel >= 0 && rel < 32) F4 &= ~(1u << ((rel & 7) * 4 + 3 - (rel >> 3)));
@@ -743,13 +780,27 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
   // vs 58.55 with four; config5 609 vs 624 ms with four instead of two;
   // still one 1 KiB block read per trip)
   constexpr int kTrips = KPL == 1 ? 2 : 4;
+  if constexpr (T15) {     // (no optimistic passes: hold is false)
+#pragma unroll kTrips
+    for (int tr = 0; tr < 8; tr += kEpi1) {
+      const int b0 = tr * G::TRIP_DW;
+      uint4 a[kEpi1];
+#pragma unroll
+      for (int i = 0; i < kEpi1; ++i)
+        a[i] = *reinterpret_cast<const uint4*>(acc + b0 + i * G::TRIP_DW + trip_lane<2, T15>(lane));
+      zero_trip<2, T15>(acc, b0, lane);
+#pragma unroll
+      for (int i = 0; i < kEpi1; ++i) block(a[i], tr + i);
+    }
+    return;
+  }
 #pragma unroll kTrips
   for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4 * kEpi1) {
     uint4 a[kEpi1];
 #pragma unroll
     for (int i = 0; i < kEpi1; ++i)
       a[i] = *reinterpret_cast<const uint4*>(acc + b0 + i * kWave * 4 + lane * 4);
-    zero_trip(acc, b0, lane);
+    zero_trip<2, T15>(acc, b0, lane);
 #pragma unroll
     for (int i = 0; i < kEpi1; ++i) {
       const int blk = (b0 >> 8) + i;
@@ -782,14 +833,141 @@ __device__ __forceinline__ void epi1_u4(const CctParams& p, uint32_t* acc, TopK<
   }
 }
 
+// Sparse epilogue (round 6; built, exact, measured slower -- off).  38 % of
+// config3's accumulator passes scatter at most 64 chunks (one load; 67 % at most
+// 192), yet the dense epilogue reads and zeroes the whole 8 KiB whatever the
+// pass scattered (profiles/r06/c/lean_phases.txt: ~11-12 k epilogue cycles per
+// pass at 1-16 chunks as at 193-384).  A one-load stage instead exchanges every
+// dword its own entries addressed with 0 (ds_wrxchg_rtn_b32, four of a chunk's
+// eight entries in flight at once): each nonzero dword comes back to exactly
+// one (lane, entry) -- a second entry or a second lane on the same dword gets
+// 0 -- so every target of the tile is judged once, and since the accumulator
+// was all zero before the stage's scatter, every dword it touched is zero
+// again after.  Dead lanes (kDeadChunk) address dword L and judge whatever it
+// holds, which is just as exact.  Thresholds per 1 KiB segment (2048 4-bit /
+// 1024 u8 targets) come from two wave-uniform words of byte-packed m_s (0:
+// above the counter width).  Same digest on all 1 M config3 rows, but 63.7 ms
+// against 58.9: the stage's chunks are only in registers until
+// the next stage's first loads reuse B, so the sparse stage issues those after
+// its epilogue and the scatter then waits out their latency, which the dense
+// epilogue hides; holding the chunks or reloading them across the transition
+// spills 46-52 VGPRs (84.5 ms).  DPS_SPARSE_LOADS=1 compiles it in.
+#ifndef DPS_SPARSE_LOADS
+#define DPS_SPARSE_LOADS 0
+#endif
+constexpr int kSparseLoads = DPS_SPARSE_LOADS;   // 0: dense epilogue only
+
+// Per-target flags of one dword against a lane's own threshold m: 4-bit
+// counters (bit 4j+3 for target j: the nibbles spread to bytes, nib + 128 - m
+// sets bit 7 exactly when nib >= m, no carry between bytes) or u8 counters
+// (bit 8j+7: the two SWAR forms of ge_u8, chosen per lane).  m = 0: none.
+__device__ __forceinline__ uint32_t sparse_flags(uint32_t v, uint32_t m, bool u8f) {
+  uint32_t f;
+  if (u8f) {
+    const uint32_t lo = v & 0x7F7F7F7Fu;
+    const uint32_t rA = v | (lo + (128u - m) * 0x01010101u);
+    const uint32_t rB = v & (lo + ((256u - m) & 0xFFu) * 0x01010101u);
+    f = (m <= 128u ? rA : rB) & 0x80808080u;
+  } else {
+    const uint32_t K = (128u - m) * 0x01010101u;
+    const uint32_t lo = v & 0x0F0F0F0Fu, hi = (v >> 4) & 0x0F0F0F0Fu;
+    f = (((lo + K) & 0x80808080u) >> 4) | ((hi + K) & 0x80808080u);
+  }
+  return m != 0u ? f : 0u;
+}
+
+template <int KPL, bool HV, bool SY>
+__device__ __forceinline__ void epi1_sparse(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
+                                            const uint4 e, int t, bool u8f, int lane,
+                                            int x_lab, int64_t gx, int mseg, int c, uint32_t hv,
+                                            uint64_t hm, RowAux& ra) {
+  const uint32_t mu = static_cast<uint32_t>(mseg);
+  const uint32_t ms = mu <= (u8f ? 255u : 15u) ? mu : 0u;
+  uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    mlo |= static_cast<uint32_t>(readlane(ms, s)) << (8 * s);
+    mhi |= static_cast<uint32_t>(readlane(ms, s + 4)) << (8 * s);
+  }
+  const int sh = u8f ? Fmt<1>::S : Fmt<2>::S;
+  const int tile_base = t << sh;                           // labels < 2^31
+  const int tpd_sh = u8f ? 2 : 3;                          // log2(targets per dword)
+  const int xr0 = x_lab - tile_base;
+  const bool xin = static_cast<uint32_t>(xr0) < (1u << sh);   // the source is a target here
+  char* const accb = reinterpret_cast<char*>(acc);
+  {
+    // two halves of four entries each (four exchanges in flight, then their
+    // judging: eight at once held 49 more VGPRs than the kernel has)
+#pragma unroll 1
+    for (int hf = 0; hf < 2; ++hf) {
+      const uint32_t wa = hf ? e.z : e.x;
+      const uint32_t wb = hf ? e.w : e.y;
+      auto addr = [&](int i) -> uint32_t {                 // the entry's dword, byte address
+        const uint32_t w = i < 2 ? wa : wb;
+        return ((i & 1) ? (w >> 19) : (w >> 3)) & kLabMask1;
+      };
+      if ((mlo | mhi) == 0u) {                             // nothing can reach a threshold
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<uint32_t*>(accb + addr(i)) = 0u;
+        continue;
+      }
+      uint32_t v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        v[i] = __hip_atomic_exchange(reinterpret_cast<uint32_t*>(accb + addr(i)), 0u,
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      auto flags = [&](int i) -> uint32_t {
+        const uint32_t a = addr(i);
+        const uint32_t seg = a >> 10;
+        const uint32_t mw = seg < 4u ? mlo : mhi;
+        uint32_t f = sparse_flags(v[i], (mw >> ((seg & 3u) << 3)) & 0xFFu, u8f);
+        if (__builtin_expect(xin, false)) {                // the source itself never counts
+          const int rel = xr0 - static_cast<int>((a >> 2) << tpd_sh);
+          if (static_cast<uint32_t>(rel) < (1u << tpd_sh)) f &= ~(1u << (u8f ? 8 * rel + 7 : 4 * rel + 3));
+        }
+        return f;
+      };
+      const uint32_t any = flags(0) | flags(1) | flags(2) | flags(3);
+      if (!ballot(any != 0u)) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint32_t f = flags(i);
+        if (!ballot(f != 0u)) continue;
+        const int lab0 = tile_base + static_cast<int>((addr(i) >> 2) << tpd_sh);
+        for (;;) {
+          const bool has = f != 0u;
+          const uint64_t mk = ballot(has);
+          if (!mk) break;
+          // every lane extracts (as in epi1_u4: no exec-mask branch per round)
+          const int bit = __builtin_ffs(static_cast<int>(f)) - 1;
+          f &= f - 1u;
+          const int j = u8f ? (bit >> 3) & 3 : (bit >> 2) & 7;
+          const int mv = static_cast<int>((v[i] >> (j << (u8f ? 3 : 2))) & (u8f ? 0xFFu : 0xFu));
+          vq_push(Q, has, lab0 + j, mv, mk, lane);
+          if (Q.n >= kWave) vq_flush<KPL, HV, SY>(p, Q, top, kWave, gx, lane, c, hv, hm, ra);
+        }
+      }
+    }
+  }
+}
+
 // Wide passes of the 4-bit format (lnp 1..3: u8 / u16 / u32 counters over a
 // half / quarter / eighth of the tile per pass), one entry at a time; padding
 // codes (e >= 2 at l % 8 == 7) add nothing.
+// (T15: passes of 15360 >> lnp targets, found by a division -- a rare path)
+template <bool T15>
 __device__ __forceinline__ void acc_add4(uint32_t* acc, uint32_t h, int c, int lnp, int pass) {
   const uint32_t e = h & 3u, yl = h >> 2;
   if ((yl & 7u) == 7u && e >= 2u) return;
-  if (static_cast<int>(yl >> (14 - lnp)) != pass) return;
-  const uint32_t local = yl & ((1u << (14 - lnp)) - 1u);
+  uint32_t local;
+  if constexpr (T15) {
+    const uint32_t pw = 15360u >> lnp, ps = yl / pw;
+    if (static_cast<int>(ps) != pass) return;
+    local = yl - ps * pw;
+  } else {
+    if (static_cast<int>(yl >> (14 - lnp)) != pass) return;
+    local = yl & ((1u << (14 - lnp)) - 1u);
+  }
   const int bits = 4 << lnp;
   const int tpds = 3 - lnp;                          // log2(targets per dword)
   const uint32_t val = static_cast<uint32_t>(c) << e;
@@ -797,10 +975,25 @@ __device__ __forceinline__ void acc_add4(uint32_t* acc, uint32_t h, int c, int l
   __hip_atomic_fetch_add(acc + (local >> tpds), add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// T15 u8-format wide passes (u16 / u32 counters over halves / quarters of a
+// 7680-target tile): one entry (label << 3 | e), padding codes add nothing.
+__device__ __forceinline__ void acc_add8w(uint32_t* acc, uint32_t h, int c, int lnp, int pass) {
+  const uint32_t e = h & 7u, yl = (h >> 3) & 0x1FFFu;
+  if ((yl & 3u) == 3u && e >= 6u) return;
+  const uint32_t val = static_cast<uint32_t>(c) << e;
+  if (val == 0) return;
+  const uint32_t pw = 7680u >> lnp, ps = yl / pw;
+  if (static_cast<int>(ps) != pass) return;
+  const uint32_t local = yl - ps * pw;
+  uint32_t* dst = lnp == 1 ? acc + (local >> 1) : acc + local;
+  const uint32_t add = lnp == 1 ? val << ((local & 1u) << 4) : val;
+  __hip_atomic_fetch_add(dst, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // A batch into the accumulator: the base pass branch-free over the loads
 // batch b issued (the u8 / 4-bit adds: dead lanes add 0, see kDeadChunk),
 // wide passes entry by entry (u8h: u8-format entries).
-template <int F>
+template <int F, bool T15>
 __device__ __forceinline__ void scatter_f(const Batch& B, const Stage& S, int b, uint32_t* acc,
                                           bool u8h) {
   if (S.lnp == 0) {                                    // u8 or 4-bit base pass
@@ -817,7 +1010,20 @@ __device__ __forceinline__ void scatter_f(const Batch& B, const Stage& S, int b,
     return;
   }
   if (F == 1 || u8h) {                                 // u8-format wide passes
-    scatter<true>(B, S, acc, Fmt<1>::S);
+    if constexpr (T15) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (B.c[u] == 0) continue;
+        const uint32_t w4[4] = {B.e[u].x, B.e[u].y, B.e[u].z, B.e[u].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc_add8w(acc, w4[q] & 0xFFFFu, B.c[u], S.lnp, S.pass);
+          acc_add8w(acc, w4[q] >> 16, B.c[u], S.lnp, S.pass);
+        }
+      }
+    } else {
+      scatter<true>(B, S, acc, Fmt<1>::S);
+    }
     return;
   }
 #pragma unroll
@@ -826,8 +1032,8 @@ __device__ __forceinline__ void scatter_f(const Batch& B, const Stage& S, int b,
     const uint32_t w4[4] = {B.e[u].x, B.e[u].y, B.e[u].z, B.e[u].w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      acc_add4(acc, w4[q] & 0xFFFFu, B.c[u], S.lnp, S.pass);
-      acc_add4(acc, w4[q] >> 16, B.c[u], S.lnp, S.pass);
+      acc_add4<T15>(acc, w4[q] & 0xFFFFu, B.c[u], S.lnp, S.pass);
+      acc_add4<T15>(acc, w4[q] >> 16, B.c[u], S.lnp, S.pass);
     }
   }
 }
@@ -835,21 +1041,22 @@ __device__ __forceinline__ void scatter_f(const Batch& B, const Stage& S, int b,
 // u8 epilogue over the whole tile: 8 blocks of 1024 targets (one threshold
 // segment each, lane l reads dwords 4l..4l+3 of the block), read and zeroed 4
 // at a time; candidates are queued and scored 64 at a time by flush().
-template <int KPL, bool HV, bool SY>
+// T15: W = 7680, 8 trips of 960 targets over lanes 0..59.
+template <int KPL, bool HV, bool SY, bool T15>
 __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<KPL>& top, VQ& Q,
                                         int t, int lane, int x_lab, int64_t gx, int mseg,
                                         int c, uint32_t hv, uint64_t hm, RowAux& ra) {
-  constexpr int kS1 = Fmt<1>::S, kSeg1 = Fmt<1>::SEG;
-  constexpr uint32_t kW1 = 1u << kS1;
-  const int tile_base = t << kS1;                        // labels < 2^31
+  using G = Geo<1, T15>;
+  const int tile_base = t * G::W;                        // labels < 2^31
   const int xr = x_lab - tile_base;
-  const bool xin = static_cast<uint32_t>(xr) < kW1;     // the source is a target of this tile
+  const bool xin = static_cast<uint32_t>(xr) < static_cast<uint32_t>(G::W);   // the source is a target here
   const int xrel = xin ? xr : 0;
+  const uint32_t lmask = trip_mask<1, T15>(lane);        // (all ones unless T15)
   // prefilter masks of the 8 segments, lane s (as in epi1_u4; 0 when m_s > 255)
   const uint32_t mu = static_cast<uint32_t>(mseg);
   const uint32_t pmv = mu > 255u ? 0u : (0x100u - (0x80000000u >> __builtin_clz(mu | 1u))) * 0x01010101u;
   auto block = [&](uint4 a, int blk) {
-    const uint32_t pm = static_cast<uint32_t>(readlane(pmv, blk));
+    const uint32_t pm = static_cast<uint32_t>(readlane(pmv, blk)) & lmask;
     if (kProfile && pm == 0u) {                    // threshold above the counter width
       ++ra.bk[0];
       return;
@@ -869,8 +1076,9 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
       F = ge_u8(a.x, kA, kB, false) | (ge_u8(a.y, kA, kB, false) >> 1) |
           (ge_u8(a.z, kA, kB, false) >> 2) | (ge_u8(a.w, kA, kB, false) >> 3);
     }
+    F &= lmask;
     // target (4*dw + byte) of this lane's 16 -> bit 8*byte + 7 - dw
-    const int i0 = (blk << kSeg1) + (lane << 4);
+    const int i0 = blk * G::SEGW + (lane << 4);
     if (__builtin_expect(xin, false)) {           // the source itself never counts
       const int rel = xrel - i0;
       if (rel >= 0 && rel < 16) F &= ~(1u << ((rel & 3) * 8 + 7 - (rel >> 2)));
@@ -899,13 +1107,27 @@ __device__ __forceinline__ void epi1_u8(const CctParams& p, uint32_t* acc, TopK<
     }
   };
   // four trips per loop iteration (round 5: 58.2 vs 58.8 ms with two)
+  if constexpr (T15) {
+#pragma unroll 4
+    for (int tr = 0; tr < 8; tr += kEpi1) {
+      const int b0 = tr * G::TRIP_DW;
+      uint4 a[kEpi1];
+#pragma unroll
+      for (int i = 0; i < kEpi1; ++i)
+        a[i] = *reinterpret_cast<const uint4*>(acc + b0 + i * G::TRIP_DW + trip_lane<1, T15>(lane));
+      zero_trip<1, T15>(acc, b0, lane);
+#pragma unroll
+      for (int i = 0; i < kEpi1; ++i) block(a[i], tr + i);
+    }
+    return;
+  }
 #pragma unroll 4
   for (int b0 = 0; b0 < kAcc1; b0 += kWave * 4 * kEpi1) {
     uint4 a[kEpi1];
 #pragma unroll
     for (int i = 0; i < kEpi1; ++i)
       a[i] = *reinterpret_cast<const uint4*>(acc + b0 + i * kWave * 4 + lane * 4);
-    zero_trip(acc, b0, lane);
+    zero_trip<1, T15>(acc, b0, lane);
 #pragma unroll
     for (int i = 0; i < kEpi1; ++i) block(a[i], (b0 >> 8) + i);
   }
@@ -1026,7 +1248,25 @@ __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __
       const int pre_n = js + 1 < kWave ? __shfl(S.G.pre, js + 1, kWave) : S.G.nq;
       const uint32_t lo_j = base_j + 4u * static_cast<uint32_t>(pre_j);
       const uint32_t len_j = 4u * static_cast<uint32_t>(pre_n - pre_j);
-      DPS_DASSERT(!live || (jt >= 0 && bj == base_j && off - lo_j < len_j));
+      // (recorded, not trapped: counter[48..55] = line, q, off, bj, base_j,
+      // pre_j, pre_n, nq of the first failing lane; tools/debug_checks.py)
+      // (bitwise, not short-circuit: the bpermutes above must run on every
+      // lane -- sunk into a branch over the live lanes, -O1 code read 0 from
+      // the lanes it had switched off and recorded false failures)
+      const bool ok_lane = (jt >= 0) & (bj == base_j) & (off - lo_j < len_j);
+      const bool bad = live & !ok_lane;
+      if (bad) {
+        unsigned long long* ctr = kcold(counter);
+        if (atomicCAS(ctr + 48, 0ull, static_cast<unsigned long long>(__LINE__)) == 0ull) {
+          ctr[49] = static_cast<unsigned long long>(q);
+          ctr[50] = off;
+          ctr[51] = bj;
+          ctr[52] = base_j;
+          ctr[53] = static_cast<unsigned long long>(pre_j);
+          ctr[54] = static_cast<unsigned long long>(pre_n);
+          ctr[55] = static_cast<unsigned long long>(S.G.nq) | (static_cast<unsigned long long>(jt + 1) << 32);
+        }
+      }
     }
 #endif
     const uint4* src = live ? reinterpret_cast<const uint4*>(ent + off) : kDeadChunk + lane;
@@ -1040,7 +1280,7 @@ __device__ __forceinline__ void issue1(const Stage& S, int b, const uint32_t* __
 
 // Venues 64.. of a row with more than 64 venues: their buckets of tile t,
 // loaded and scattered synchronously (pass `pass` of mode lnp).
-template <int F>
+template <int F, bool T15>
 __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, uint32_t* acc,
                                             int64_t pb, int d, int lane, bool u8h) {
   const uint32_t* off = u8h ? p.h_off : p.tile_off;
@@ -1064,7 +1304,7 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
     for (int b = 0; b < E.nb; ++b) {
       Batch B;
       issue1(E, b, ent, lane, B);
-      scatter_f<F>(B, E, b, acc, u8h);
+      scatter_f<F, T15>(B, E, b, acc, u8h);
     }
   }
   return chunks;
@@ -1084,7 +1324,7 @@ __device__ __forceinline__ int extra_groups(const CctParams& p, const Stage& S, 
 // extra_groups and the row loop).  Do not add a kernel argument or call a
 // kcold-using helper from another kernel.
 static_assert(std::is_trivially_copyable<CctParams>::value, "CctParams is passed by value");
-template <int F, int KPL, bool HV, bool SY, bool OPT>
+template <int F, int KPL, bool HV, bool SY, bool OPT, bool T15>
 // The symmetric-mode instantiation carries the record path and the published
 // bounds: DPS_SYM_WPE waves per SIMD (4: 128 VGPRs, no spills).
 #ifndef DPS_SYM_WPE
@@ -1094,18 +1334,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
     SY ? DPS_SYM_WPE : KPL <= DPS_W5_KPL ? 5 : 4))) void k_cct1(CctParams p) {
   // LDS: the accumulator at address 0 (scatter ORs the in-tile offset into 0)
   // then the candidate queue.
-  __shared__ __attribute__((aligned(16))) uint32_t lds[kAcc1];
+  static_assert(!T15 || (!SY && !OPT), "the T15 layout has no symmetric or optimistic passes");
+  __shared__ __attribute__((aligned(16))) uint32_t lds[Geo<F, T15>::ACC_DW];
   uint32_t* acc = lds;
   const int lane = lane_id();
   VQ Q;
   Q.lab0 = Q.m0 = Q.lab1 = Q.m1 = 0;
   Q.n = 0;
-  for (int i = lane * 4; i < kAcc1; i += kWave * 4)
+  for (int i = lane * 4; i < Geo<F, T15>::ACC_DW; i += kWave * 4)
     *reinterpret_cast<uint4*>(acc + i) = make_uint4(0, 0, 0, 0);
   // profiling aid (-DDPS_PROFILE build, DPATHSIM_ABLATE=16): shader-clock
   // cycles per phase (scatter, flush + thresholds, next-stage prefetch,
   // epilogue) and the stage count, summed over waves into counter[8..12]
   const bool prof = kProfile && (p.ablate & 16) != 0;
+  // profiling build: this wave's realtime stamps (100 MHz, chip-wide), at
+  // counter[64 + 4 * wave]: start, end, start of its last row, that row
+  const uint64_t rt0 = prof ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint64_t rt_last = 0;
+  int x_last = -1;
   uint64_t ts[7] = {0, 0, 0, 0, 0, 0, 0}, pc[7] = {0, 0, 0, 0, 0, 0, 0};
   // work counts of this wave (wave-uniform), summed into counter[1..2] at exit:
   // accumulator passes (each reads and zeroes the 8 KiB accumulator) and 16-byte
@@ -1120,6 +1366,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
     if (r >= kcold(n_rows)) break;
     const int32_t* row_order = kcold(row_order);
     const int x = row_order ? row_order[r] : static_cast<int>(kcold(row_begin) + r);   // < 2^31
+    if (prof) {
+      rt_last = __builtin_amdgcn_s_memrealtime();
+      x_last = r;
+    }
     const bool is_piece = r < kcold(n_pieces);
     int t_beg = is_piece ? kcold(piece_t0)[r] : 0;
     int t_end = is_piece ? kcold(piece_t1)[r] : static_cast<int>(p.T);
@@ -1246,7 +1496,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       choose(-1.0, t0, ub_t, u8n, optn, hb_t);
       if (t0 >= 0) {
         Pend1 P;
-        pend_load<F, HV, SY>(p, P, t0, ub_t, u8n, d0, vT, vT8, lane, ra.far, optn, hb_t);
+        pend_load<F, HV, SY, T15>(p, P, t0, ub_t, u8n, d0, vT, vT8, lane, ra.far, optn, hb_t);
         Stage1 X;
         stage_make<F>(X, P, c, d0, 0ull, lane);
         bool hchg = false;        // H grew at the last stage boundary
@@ -1254,7 +1504,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
         issue1(X.S, 0, X.u8h ? p.h_ent : p.tile_ent, lane, B);
         int t1;
         choose(-1.0, t1, ub_t, u8n, optn, hb_t);
-        pend_load<F, HV, SY>(p, P, t1, ub_t, u8n, d0, vT, vT8, lane, ra.far, optn, hb_t);
+        pend_load<F, HV, SY, T15>(p, P, t1, ub_t, u8n, d0, vT, vT8, lane, ra.far, optn, hb_t);
         for (;;) {
           const int npass = 1 << X.S.lnp;
           bool more = false;
@@ -1262,16 +1512,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
             if (prof) ts[0] = __builtin_amdgcn_s_memtime();
             const uint32_t* ent = X.u8h ? p.h_ent : p.tile_ent;
             if (X.S.pass > 0) issue1(X.S, 0, ent, lane, B);
-            scatter_f<F>(B, X.S, 0, acc, X.u8h);
+            scatter_f<F, T15>(B, X.S, 0, acc, X.u8h);
             for (int b = 1; b < X.S.nb; ++b) {
               Batch B2;
               issue1(X.S, b, ent, lane, B2);
-              scatter_f<F>(B2, X.S, b, acc, X.u8h);
+              scatter_f<F, T15>(B2, X.S, b, acc, X.u8h);
             }
             n_chunk += static_cast<uint32_t>(X.S.G.nq);
             ++n_pass;
             if (d > kWave)
-              n_chunk += static_cast<uint32_t>(extra_groups<F>(p, X.S, acc, pb, d, lane, X.u8h));
+              n_chunk += static_cast<uint32_t>(extra_groups<F, T15>(p, X.S, acc, pb, d, lane, X.u8h));
             if (prof) ts[1] = __builtin_amdgcn_s_memtime();
             // score what is queued while the list is filling or the queue is
             // half full (one memory round trip per 64 candidates)
@@ -1309,6 +1559,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
               mseg = min(mseg, my > 1 ? my : 1);
             }
             const bool last = X.S.pass + 1 == npass;
+            // a one-load stage: the sparse epilogue (DPS_SPARSE_LOADS, off), run
+            // after the transition while B still holds this stage's chunks
+            const bool sparse = kSparseLoads > 0 && !T15 && !SY && !(OPT && X.opt) && X.S.lnp == 0 &&
+                                d <= kWave && X.S.G.nq <= kWave;
             Stage S = X.S;
             const bool u8S = F == 1 || X.u8h;   // this stage's counters: u8 format
             const bool S_u8h = X.u8h;
@@ -1354,12 +1608,20 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
                 X.opt = false;
               }
               if (prof) ts[5] = __builtin_amdgcn_s_memtime();
-              issue1(X.S, 0, X.u8h ? p.h_ent : p.tile_ent, lane, B);
+              // (a sparse stage issues the next batch after its epilogue: B
+              // still holds this stage's chunks)
+              if (!sparse) issue1(X.S, 0, X.u8h ? p.h_ent : p.tile_ent, lane, B);
               if (prof) ts[6] = __builtin_amdgcn_s_memtime();
               int tn = -1;
               if (more) choose(tau, tn, ub_t, u8n, optn, hb_t);
-              pend_load<F, HV, SY>(p, P, tn, ub_t, u8n, d0, vT, vT8, lane, ra.far, optn, hb_t);
+              pend_load<F, HV, SY, T15>(p, P, tn, ub_t, u8n, d0, vT, vT8, lane, ra.far, optn, hb_t);
             }
+            if (sparse) {
+              epi1_sparse<KPL, HV, SY>(p, acc, top, Q, B.e[0], static_cast<int>(S.t), u8S, lane,
+                                       x_lab, gx, mseg, c, hv, hmS, ra);
+              issue1(X.S, 0, X.u8h ? p.h_ent : p.tile_ent, lane, B);
+            }
+
             // which halves of an optimistic pass have a count that reached 16?
             // (the epilogue clears them without judging them; they run again
             // as their u8 half tiles, queued for a later stage)
@@ -1383,17 +1645,19 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
             }
 #endif
             if (prof) ts[3] = __builtin_amdgcn_s_memtime();
-            if (S.lnp == 0) {
+            if (sparse) {
+              // (judged and cleared above)
+            } else if (S.lnp == 0) {
               if (u8S)
-                epi1_u8<KPL, HV, SY>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
+                epi1_u8<KPL, HV, SY, T15>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
                                  hmS, ra);
               else
-                epi1_u4<KPL, HV, SY>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
+                epi1_u4<KPL, HV, SY, T15>(p, acc, top, Q, static_cast<int>(S.t), lane, x_lab, gx, mseg, c, hv,
                                  hmS, ra, bmask, oexp, bad);
             } else if (u8S) {
-              epi1_wide<1, KPL, HV, SY>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, ra);
+              epi1_wide<1, KPL, HV, SY, T15>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, ra);
             } else {
-              epi1_wide<F, KPL, HV, SY>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, ra);
+              epi1_wide<F, KPL, HV, SY, T15>(p, acc, top, Q, S, lane, x_lab, gx, mseg, c, hv, hmS, ra);
             }
             if (OPT && bad) {
               // halves of an optimistic pass with a count that reached 16: run
@@ -1469,7 +1733,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       for (int q = 0; q < KPL; ++q) {
         for (int l = 0; l < kWave; ++l) {
           if (q * kWave + l >= top.filled) break;
+#ifdef DPS_DEBUG
+          // (the readlane outside the short-circuit: under it the -O1 debug
+          // build read lanes whose ranked entry had never been loaded)
+          const int yl = readlane(top.y[q], l);
+          ok = ok && yl != static_cast<int>(yc);
+#else
+          // (the same at -O3, where this form allocates better: 58.0 vs 58.8 ms
+          // for the whole config3 launch, profiles/r06/f)
           ok = ok && (readlane(top.y[q], l) != static_cast<int>(yc));
+#endif
         }
       }
       const uint64_t mk = ballot(ok);
@@ -1495,6 +1768,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
     if (HV && ra.ver) atomicAdd(ctr + 3, static_cast<unsigned long long>(ra.ver));
     if (ra.redo) atomicAdd(ctr + 4, static_cast<unsigned long long>(ra.redo));
   }
+  if (prof && lane == 0 && blockIdx.x < 16384) {
+    unsigned long long* wt = p.counter + 64 + 4 * static_cast<int64_t>(blockIdx.x);
+    wt[0] = rt0;
+    wt[1] = __builtin_amdgcn_s_memrealtime();
+    wt[2] = rt_last;
+    wt[3] = static_cast<unsigned long long>(static_cast<long long>(x_last));
+  }
   if (prof && lane == 0) {
 #pragma unroll
     for (int i = 0; i < 7; ++i) atomicAdd(p.counter + 8 + i, static_cast<unsigned long long>(pc[i]));
@@ -1513,25 +1793,36 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
   }
 }
 
-template <int F, int KPL>
+template <int F, int KPL, bool T15>
 int launch1(const CctParams& p, hipStream_t st) {
   int dev = 0, n_cu = 256;
   DPS_HIP_RET(hipGetDevice(&dev));
   DPS_HIP_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-  int wpc = KPL <= DPS_W5_KPL ? 20 : 16;   // 5 or 4 waves per SIMD, 8 KB of LDS each
+  // 5 or 4 waves per SIMD by registers; the 8 KiB layout keeps 18 resident per
+  // CU by LDS (Geo), the T15 layout 20 (a grid of 20 measured the same as 18
+  // for 8 KiB: the two late workgroups per CU start at the end, profiles/r06/h)
+  int wpc = KPL <= DPS_W5_KPL ? (T15 ? 20 : 18) : 16;
   if (p.sym) wpc = 4 * (DPS_SYM_WPE < (KPL <= DPS_W5_KPL ? 5 : 4) ? DPS_SYM_WPE : (KPL <= DPS_W5_KPL ? 5 : 4));
+  if (const int t = tuning(DPS_TUNE_LEAN_WPC)) wpc = t;   // A/B of the occupancy
 #ifdef DPS_PROFILE
   if (const char* e = std::getenv("DPATHSIM_LEAN_WPC")) wpc = std::atoi(e);   // experiments
   if (wpc < 1 || wpc > 20) wpc = 20;
 #endif
   int64_t grid = static_cast<int64_t>(n_cu) * wpc;
   if (grid > p.n_rows) grid = p.n_rows;
+  const auto g = static_cast<unsigned>(grid);
+  if constexpr (T15) {        // (the caller rejects sym and tile_sum for this layout)
+    if (p.hv_c) k_cct1<F, KPL, true, false, false, true><<<g, kWave, 0, st>>>(p);
+    else k_cct1<F, KPL, false, false, false, true><<<g, kWave, 0, st>>>(p);
+    DPS_LAUNCHED();
+    return DPS_OK;
+  }
   const bool opt = F == 2 && p.tile_sum != nullptr && p.h_ent != nullptr && kOptMax > 0;
-  if (p.sym) k_cct1<F, KPL, false, true, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
-  else if (p.hv_c && opt) k_cct1<F, KPL, true, false, true><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
-  else if (p.hv_c) k_cct1<F, KPL, true, false, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
-  else if (opt) k_cct1<F, KPL, false, false, true><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
-  else k_cct1<F, KPL, false, false, false><<<static_cast<unsigned>(grid), kWave, 0, st>>>(p);
+  if (p.sym) k_cct1<F, KPL, false, true, false, false><<<g, kWave, 0, st>>>(p);
+  else if (p.hv_c && opt) k_cct1<F, KPL, true, false, true, false><<<g, kWave, 0, st>>>(p);
+  else if (p.hv_c) k_cct1<F, KPL, true, false, false, false><<<g, kWave, 0, st>>>(p);
+  else if (opt) k_cct1<F, KPL, false, false, true, false><<<g, kWave, 0, st>>>(p);
+  else k_cct1<F, KPL, false, false, false, false><<<g, kWave, 0, st>>>(p);
   DPS_LAUNCHED();
   return DPS_OK;
 }
@@ -1542,15 +1833,26 @@ int launch1(const CctParams& p, hipStream_t st) {
 // 4-bit counters), one wave per row; the caller has validated the parameters
 // and zeroed p.counter.
 int cct1_launch(const CctParams& p, hipStream_t st) {
+  const bool t15 = p.tile_w != (1 << p.shift);
+  if (p.shift == 13 && t15) {
+    if (p.k <= 64) return launch1<1, 1, true>(p, st);
+    if (p.k <= 128) return launch1<1, 2, true>(p, st);
+    return launch1<1, 4, true>(p, st);
+  }
+  if (p.shift == 14 && t15) {
+    if (p.k <= 64) return launch1<2, 1, true>(p, st);
+    if (p.k <= 128) return launch1<2, 2, true>(p, st);
+    return launch1<2, 4, true>(p, st);
+  }
   if (p.shift == 13) {
-    if (p.k <= 64) return launch1<1, 1>(p, st);
-    if (p.k <= 128) return launch1<1, 2>(p, st);
-    return launch1<1, 4>(p, st);
+    if (p.k <= 64) return launch1<1, 1, false>(p, st);
+    if (p.k <= 128) return launch1<1, 2, false>(p, st);
+    return launch1<1, 4, false>(p, st);
   }
   if (p.shift == 14) {
-    if (p.k <= 64) return launch1<2, 1>(p, st);
-    if (p.k <= 128) return launch1<2, 2>(p, st);
-    return launch1<2, 4>(p, st);
+    if (p.k <= 64) return launch1<2, 1, false>(p, st);
+    if (p.k <= 128) return launch1<2, 2, false>(p, st);
+    return launch1<2, 4, false>(p, st);
   }
   return DPS_ERR_INVALID;
 }

@@ -24,7 +24,9 @@ struct CctParams {
   const int64_t* tile_gmin;
   int64_t n_targets;
   int64_t T;
-  int shift;
+  int shift;                 // the entry format: 13 u8, 14 4-bit, 15-16 32-bit entries
+  int tile_w;                // targets per tile: 2^shift, or 15 * 2^(shift - 4) (the T15
+                             // layout of dps_cct1.hip: 7680 u8 / 15360 4-bit)
   int64_t row_begin;
   const int32_t* row_order;  // nullable: dequeue order of the rows (e.g. heaviest first)
   bool out_by_slot;          // output row = dequeue slot (dps_cct_topk_rows), else x - row_begin
@@ -109,6 +111,12 @@ namespace {
 constexpr bool kProfile = true;
 #else
 constexpr bool kProfile = false;
+#endif
+// The device-assert debug build (make debug, -DDPS_DEBUG).
+#ifdef DPS_DEBUG
+constexpr bool kDebug = true;
+#else
+constexpr bool kDebug = false;
 #endif
 
 // Waves per workgroup NW is a template parameter: 4 (256 threads) for tiles

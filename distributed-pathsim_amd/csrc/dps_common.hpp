@@ -13,6 +13,33 @@ namespace dps {
 
 constexpr int kWave = 64;
 
+// Target tiles of the C^T layout (dps_tiles.hip, dps_cct1.hip): W = 2^shift
+// labels for shift in [8, 16], or the T15 layout -- 15 / 16 of 8192 / 16384,
+// i.e. 7680 (u8 entries, shift 13) or 15360 (4-bit entries, shift 14), whose
+// 7680-byte accumulator keeps 20 one-wave workgroups resident on a CU (8 KiB
+// keeps 18, Geo in dps_cct1.hip).  Labels are < 2^31.
+struct TileDim {
+  int shift;   // entry format; log2(W) unless t15
+  bool t15;
+  __host__ __device__ int64_t w() const {
+    return t15 ? int64_t(15) << (shift - 4) : int64_t(1) << shift;
+  }
+  __host__ __device__ int64_t tile(int64_t lab) const {
+    return t15 ? static_cast<int64_t>(static_cast<uint32_t>(lab >> (shift - 4)) / 15u) : lab >> shift;
+  }
+  __host__ __device__ uint32_t local(int64_t lab) const {
+    return static_cast<uint32_t>(lab - tile(lab) * w());
+  }
+};
+// The tile width's TileDim; shift = -1 when the width is not one of them.
+inline TileDim tile_dim(int32_t w) {
+  if (w == 7680) return TileDim{13, true};
+  if (w == 15360) return TileDim{14, true};
+  int s = 0;
+  while (s < 31 && (1 << s) < w) ++s;
+  return TileDim{(1 << s) == w && s >= 8 && s <= 16 ? s : -1, false};
+}
+
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 // Bump allocator over the caller's workspace (never allocates device memory).

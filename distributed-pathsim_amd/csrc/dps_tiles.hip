@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
                                                        const int32_t* __restrict__ c_val,
                                                        const int32_t* __restrict__ rank,
                                                        const int64_t* __restrict__ g,
-                                                       int64_t n_rows, int shift, int64_t T,
+                                                       int64_t n_rows, TileDim td, int64_t T,
                                                        uint32_t* __restrict__ cnt,
                                                        uint32_t* __restrict__ maxc,
                                                        unsigned long long* __restrict__ gmin,
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
   for (int64_t y = wave0; y < n_rows; y += nwaves) {
-    const int64_t t = label_of(rank, y) >> shift;
+    const int64_t t = td.tile(label_of(rank, y));
     if (lane == 0 && gmin) {
       if (lds_gmin) atomicMin(&gmin_s[t], static_cast<unsigned long long>(g[y]));
       else atomicMin(&gmin[t], static_cast<unsigned long long>(g[y]));
@@ -124,8 +124,8 @@ __global__ __launch_bounds__(kBlock) void k_tile_count(const int64_t* __restrict
       const int32_t c = c_val[j];
       if (c > 0xFFFF && status) *status = DPS_ERR_OVERFLOW;
       const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
-      atomicAdd(&cnt[b], n_pieces(tile_fmt(shift), static_cast<uint32_t>(c),
-                                  static_cast<uint32_t>(label_of(rank, y))));
+      atomicAdd(&cnt[b], n_pieces(tile_fmt(td.shift), static_cast<uint32_t>(c),
+                                  td.local(label_of(rank, y))));
       // C = 1 (most entries when buckets are sparse) needs no atomic: k_round4
       // raises the maximum of every non-empty bucket to at least 1
       if (maxc && c > 1) atomicMax(&maxc[b], static_cast<uint32_t>(c));
@@ -271,22 +271,21 @@ __global__ __launch_bounds__(kBlock) void k_tile_scatter(const int64_t* __restri
                                                          const int32_t* __restrict__ c_col,
                                                          const int32_t* __restrict__ c_val,
                                                          const int32_t* __restrict__ rank,
-                                                         int64_t n_rows, int shift, int64_t T,
+                                                         int64_t n_rows, TileDim td, int64_t T,
                                                          const int64_t* __restrict__ off,
                                                          uint32_t* __restrict__ cursor,
                                                          uint32_t* __restrict__ ent) {
   const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
-  const uint32_t ymask = (1u << shift) - 1u;
   for (int64_t y = wave0; y < n_rows; y += nwaves) {
     const int64_t lab = label_of(rank, y);
-    const int64_t t = lab >> shift;
+    const int64_t t = td.tile(lab);
     for (int64_t j = c_ptr[y] + lane; j < c_ptr[y + 1]; j += kWave) {
       const int64_t b = static_cast<int64_t>(c_col[j]) * T + t;
       const uint32_t c = static_cast<uint32_t>(c_val[j]);
-      const int fmt = tile_fmt(shift);
-      const uint32_t l = static_cast<uint32_t>(lab) & ymask;
+      const int fmt = tile_fmt(td.shift);
+      const uint32_t l = td.local(lab);
       const uint32_t pos = atomicAdd(&cursor[b], n_pieces(fmt, c, l));
       put_entry(fmt, ent, off[b] + pos, c, l);
     }
@@ -556,7 +555,7 @@ __device__ __forceinline__ MidRange mid_range(int64_t r, int64_t n_mids) {
 __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
     const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
     const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm,
-    const int64_t* __restrict__ g, int64_t n_targets, int64_t n_mids, int shift, int64_t T,
+    const int64_t* __restrict__ g, int64_t n_targets, int64_t n_mids, TileDim td, int64_t T,
     int labels_per_block, int P, int S, int n_ranges, const uint32_t* __restrict__ part_n,
     uint32_t* __restrict__ cntp, uint32_t* __restrict__ mxp,
     unsigned long long* __restrict__ gmin, int32_t* __restrict__ status) {
@@ -579,10 +578,10 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_blk(
   if (static_cast<int>(sb) >= sr.n_sub) return;   // block-uniform: before any barrier
   for (int v = threadIdx.x; v < mr.n; v += kBlkThreads) { cnt_s[v] = 0; mx_s[v] = 0; }
   if (threadIdx.x == 0) { gmin_s = ~0ull; ovf_s = 0; }
-  const int fmt = tile_fmt(shift);
+  const int fmt = tile_fmt(td.shift);
   const int64_t l0 = part * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
-  const int64_t t = l0 >> shift;
+  const int64_t t = td.tile(l0);
   const int64_t h = part % P;
   __syncthreads();
   const BlockRows R{rel_s, d_s};
@@ -643,7 +642,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_parts_fix(uint32_t* __restrict_
 __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
     const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
     const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm, int64_t n_targets,
-    int64_t n_mids, int shift, int64_t T, int labels_per_block, int P, int S, int n_ranges,
+    int64_t n_mids, TileDim td, int64_t T, int labels_per_block, int P, int S, int n_ranges,
     const uint32_t* __restrict__ part_n, const int64_t* __restrict__ offp,
     uint32_t* __restrict__ curp, uint32_t* __restrict__ ent) {
   __shared__ uint32_t cnt_s[kBlkMids];
@@ -661,18 +660,17 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
   const SubRange sr = sub_range(part_n[part], sb, S);
   if (static_cast<int>(sb) >= sr.n_sub) return;   // block-uniform: before any barrier
   for (int v = threadIdx.x; v < mr.n; v += kBlkThreads) cnt_s[v] = 0;
-  const int fmt = tile_fmt(shift);
+  const int fmt = tile_fmt(td.shift);
   const int64_t l0 = part * labels_per_block;
   const int64_t l1 = min(l0 + labels_per_block, n_targets);
-  const int64_t t = l0 >> shift;
+  const int64_t t = td.tile(l0);
   const int64_t h = part % P;
-  const uint32_t ymask = (1u << shift) - 1u;
   __syncthreads();
   const BlockRows R{rel_s, d_s};
   const int nl = static_cast<int>(l1 - l0);
   stage_rows(c_ptr, perm, nullptr, l0, l1, R, wsum, nullptr);
   if (sr.e1 - sr.e0 <= kMaxStrips * kWave) strip_table(R, nl, sr.e0, sr.e1, tab_s);
-  const uint32_t lab0 = static_cast<uint32_t>(l0) & ymask;
+  const uint32_t lab0 = td.local(l0);   // (a part lies inside one tile)
   if (sr.n_sub == 1) {
     for (int lv = threadIdx.x; lv < mr.n; lv += kBlkThreads)
       base_s[lv] = static_cast<unsigned long long>(offp[((mr.m0 + lv) * T + t) * P + h]);
@@ -706,14 +704,14 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
 // Single-source dense row: one block per target tile; out_m in ORIGINAL order.
 __global__ __launch_bounds__(kBlock) void k_walk_row(const int32_t* __restrict__ src_col,
                                                      const int32_t* __restrict__ src_val,
-                                                     int64_t src_len, int64_t n_targets, int shift,
+                                                     int64_t src_len, int64_t n_targets, TileDim td,
                                                      int64_t T, const uint32_t* __restrict__ off,
                                                      const uint32_t* __restrict__ ent,
                                                      const int32_t* __restrict__ t_perm,
                                                      int64_t* __restrict__ out_m) {
   // int32 accumulators for up to 32768 labels; wider tiles run in 32768-label parts
   extern __shared__ __attribute__((aligned(16))) int32_t acc[];
-  const int W = 1 << shift;
+  const int W = static_cast<int>(td.w());
   const int P = W < 32768 ? W : 32768;
   const int64_t t = blockIdx.x;
   for (int part = 0; part < W / P; ++part) {
@@ -724,7 +722,7 @@ __global__ __launch_bounds__(kBlock) void k_walk_row(const int32_t* __restrict__
       const int cx = src_val[j];
       for (uint32_t i = off[b] + threadIdx.x; i < off[b + 1]; i += kBlock) {
         const uint32_t w = ent[i];
-        const int fmt = tile_fmt(shift);
+        const int fmt = tile_fmt(td.shift);
         if (fmt != kFmt32) {   // two 16-bit entries per word (W = P here)
           const uint32_t sh = ent_lsh(fmt);
 #pragma unroll
@@ -742,7 +740,7 @@ __global__ __launch_bounds__(kBlock) void k_walk_row(const int32_t* __restrict__
       }
     }
     __syncthreads();
-    const int64_t y0 = (t << shift) + static_cast<int64_t>(part) * P;
+    const int64_t y0 = t * W + static_cast<int64_t>(part) * P;
     for (int i = threadIdx.x; i < P && y0 + i < n_targets; i += kBlock) {
       const int64_t lab = y0 + i;
       out_m[t_perm ? t_perm[lab] : lab] = acc[i];
@@ -796,6 +794,12 @@ int log2_exact(int32_t w) {
   return (1 << s) == w ? s : -1;
 }
 
+// Label mask of the padding entries: a power of two minus one that stays
+// below the tile width (the padding labels only spread no-op adds over banks).
+uint32_t pad_mask(TileDim td) {
+  return td.t15 ? (1u << (td.shift - 1)) - 1u : (1u << td.shift) - 1u;
+}
+
 // Labels per block of the block-local build: a power of two in [1024, tile_w]
 // (DPATHSIM_TILE_LPB overrides the default in the -DDPS_PROFILE build, for A/B runs).  Every block writes
 // one count slot per (mid, part), so fewer, wider parts shrink the slot arrays
@@ -806,6 +810,7 @@ int tile_lpb(int32_t tile_w) {
   if (const char* e = std::getenv("DPATHSIM_TILE_LPB")) lpb = std::atoi(e);
 #endif
   if (lpb < 1024 || lpb > kBlkLabels || (lpb & (lpb - 1))) lpb = kBlkLabels;
+  if (tile_dim(tile_w).t15) return 3840;   // a divisor of 7680 and 15360 (parts never cross tiles)
   return tile_w < lpb ? tile_w : lpb;
 }
 
@@ -917,14 +922,13 @@ __global__ __launch_bounds__(kBlock) void k_tile_keys(const int64_t* __restrict_
                                                       const int32_t* __restrict__ c_val,
                                                       const int32_t* __restrict__ rank,
                                                       const int64_t* __restrict__ Q,
-                                                      int64_t n_rows, int shift, int64_t cap,
+                                                      int64_t n_rows, TileDim td, int64_t cap,
                                                       uint64_t* __restrict__ keys,
                                                       uint32_t* __restrict__ vals,
                                                       int32_t* __restrict__ status) {
   const int lane = lane_id();
   const int64_t wave0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * (kBlock / kWave);
-  const uint32_t ymask = (1u << shift) - 1u;
   for (int64_t r0 = wave0 * kWave; r0 < n_rows; r0 += nwaves * kWave) {
     const int64_t x = r0 + lane;
     const int64_t base = c_ptr[r0];
@@ -953,8 +957,8 @@ __global__ __launch_bounds__(kBlock) void k_tile_keys(const int64_t* __restrict_
         }
         const int64_t d = static_cast<int64_t>(qk + i);
         if (d < cap) {   // past an undersized nnz_cap: k_tile_keys_pad reports the overflow
-          keys[d] = (static_cast<uint64_t>(lb >> shift) << 32) | v;
-          vals[d] = ((lb & ymask) << 16) | c;
+          keys[d] = (static_cast<uint64_t>(td.tile(lb)) << 32) | v;
+          vals[d] = (td.local(lb) << 16) | c;
         }
       }
     }
@@ -964,10 +968,10 @@ __global__ __launch_bounds__(kBlock) void k_tile_keys(const int64_t* __restrict_
 // Tile t's smallest denominator term, one block per tile (no atomics).
 __global__ __launch_bounds__(kBlock) void k_tile_gmin(const int32_t* __restrict__ perm,
                                                       const int64_t* __restrict__ g, int64_t n_rows,
-                                                      int shift, int64_t* __restrict__ gmin) {
+                                                      TileDim td, int64_t* __restrict__ gmin) {
   __shared__ int64_t s[kBlock];
-  const int64_t lo = static_cast<int64_t>(blockIdx.x) << shift;
-  const int64_t hi = lo + (int64_t(1) << shift) < n_rows ? lo + (int64_t(1) << shift) : n_rows;
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * td.w();
+  const int64_t hi = lo + td.w() < n_rows ? lo + td.w() : n_rows;
   int64_t m = INT64_MAX;
   for (int64_t lab = lo + threadIdx.x; lab < hi; lab += kBlock) {
     const int64_t v = g[perm[lab]];
@@ -1122,7 +1126,7 @@ int64_t dps_ct_tiles_ent_capacity(int64_t nnz, int64_t sum_c, int64_t n_mids,
   if (tile_w <= 0 || nnz < 0 || sum_c < nnz) return 0;
   const int64_t T = (n_targets + tile_w - 1) / tile_w;
   const int64_t nb = n_mids * (T > 0 ? T : 1);
-  if (tile_fmt(log2_exact(tile_w)) == kFmt32) return nnz + 3 * (nb < nnz ? nb : nnz) + 4;
+  if (tile_fmt(tile_dim(tile_w).shift) == kFmt32) return nnz + 3 * (nb < nnz ? nb : nnz) + 4;
   // 16-bit entries: power-of-two pieces, at most (c + 1) / 2 <= 1 + (c - 1) / 2
   // per C entry; up to 9 padding entries per non-empty bucket; two entries per
   // uint32 word
@@ -1151,11 +1155,12 @@ size_t dps_ct_tiles_workspace_size(int64_t n_mids, int64_t n_targets, int32_t ti
 int dps_ct_tiles_sums(const uint32_t* tile_off, const uint32_t* tile_ent, int64_t n_buckets,
                       int32_t tile_w, uint32_t* tile_sum, void* stream) {
   DPS_REQUIRE(n_buckets >= 0, DPS_ERR_INVALID, "bad n_buckets");
-  DPS_REQUIRE(tile_w >= 256 && tile_w <= 65536 && (tile_w & (tile_w - 1)) == 0, DPS_ERR_INVALID,
-              "tile_w must be a power of two in [256, 65536]");
+  const TileDim td = tile_dim(tile_w);
+  DPS_REQUIRE(td.shift >= 0, DPS_ERR_INVALID,
+              "tile_w must be a power of two in [256, 65536], 7680 or 15360");
   if (n_buckets == 0) return DPS_OK;
   DPS_REQUIRE(tile_off && tile_ent && tile_sum, DPS_ERR_INVALID, "null array");
-  const int fmt = tile_fmt(log2_exact(tile_w));
+  const int fmt = tile_fmt(td.shift);
   k_tile_sums<<<grid_for(n_buckets * 16, kBlock), kBlock, 0, static_cast<hipStream_t>(stream)>>>(
       tile_off, tile_ent, n_buckets, fmt, tile_sum);
   DPS_LAUNCHED();
@@ -1167,9 +1172,10 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
                        int32_t tile_w, uint32_t* tile_off, uint32_t* tile_ent, uint32_t* tile_maxc,
                        int64_t* tile_gmin, int32_t* status_dev, void* ws, size_t ws_bytes,
                        void* stream) {
-  const int shift = log2_exact(tile_w);
+  const TileDim td = tile_dim(tile_w);
+  const int shift = td.shift;
   DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED,
-              "tile_w must be a power of two in [256, 65536], got %d", tile_w);
+              "tile_w must be a power of two in [256, 65536], 7680 or 15360, got %d", tile_w);
   DPS_REQUIRE(n_targets >= 0 && n_mids >= 0, DPS_ERR_INVALID, "negative size");
   DPS_REQUIRE(n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "n_targets exceeds int32");
   DPS_REQUIRE(!tile_gmin || g, DPS_ERR_INVALID, "tile_gmin needs g");
@@ -1239,7 +1245,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     }
     if (n_targets > 0 && nb > 0) {
       k_tile_count_blk<<<static_cast<unsigned>(nblk * S * n_ranges), kBlkThreads, 0, st>>>(
-          c_ptr, c_col, c_val, perm_or_null, tile_gmin ? g : nullptr, n_targets, n_mids, shift, T,
+          c_ptr, c_col, c_val, perm_or_null, tile_gmin ? g : nullptr, n_targets, n_mids, td, T,
           lpb, P, S, n_ranges, part_n, cntp, mxp,
           reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
       DPS_LAUNCHED();
@@ -1254,13 +1260,13 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
     DPS_LAUNCHED();
     if (n_targets > 0 && nb > 0) {
       k_tile_scatter_blk<<<static_cast<unsigned>(nblk * S * n_ranges), kBlkThreads, 0, st>>>(
-          c_ptr, c_col, c_val, perm_or_null, n_targets, n_mids, shift, T, lpb, P, S, n_ranges,
+          c_ptr, c_col, c_val, perm_or_null, n_targets, n_mids, td, T, lpb, P, S, n_ranges,
           part_n, off64, curp, tile_ent);
       DPS_LAUNCHED();
     }
     if (nb > 0) {
-      k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(
-          off64, P, cnt, nb, static_cast<uint32_t>(tile_w) - 1u, fmt, tile_ent);
+      k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(off64, P, cnt, nb, pad_mask(td), fmt,
+                                                          tile_ent);
       DPS_LAUNCHED();
     }
     return bank_order(p16, nb, tile_off, tile_ent, st);
@@ -1271,7 +1277,7 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   if (tile_maxc) DPS_HIP_RET(hipMemsetAsync(tile_maxc, 0, (nb + 1) * sizeof(uint32_t), st));
   if (n_targets > 0 && nb > 0) {
     k_tile_count<<<grid_for(n_targets * kWave, kBlock, 2048), kBlock, 0, st>>>(
-        c_ptr, c_col, c_val, t_rank, g, n_targets, shift, T, cnt, tile_maxc,
+        c_ptr, c_col, c_val, t_rank, g, n_targets, td, T, cnt, tile_maxc,
         reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
     DPS_LAUNCHED();
   }
@@ -1284,12 +1290,12 @@ int dps_ct_tiles_build(const int64_t* c_ptr, const int32_t* c_col, const int32_t
   DPS_LAUNCHED();
   if (n_targets > 0 && nb > 0) {
     k_tile_scatter<<<grid_for(n_targets * kWave, kBlock), kBlock, 0, st>>>(
-        c_ptr, c_col, c_val, t_rank, n_targets, shift, T, off64, cursor, tile_ent);
+        c_ptr, c_col, c_val, t_rank, n_targets, td, T, off64, cursor, tile_ent);
     DPS_LAUNCHED();
   }
   if (nb > 0) {
-    k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(
-        off64, 1, cursor, nb, static_cast<uint32_t>(tile_w) - 1u, fmt, tile_ent);
+    k_tile_pad<<<grid_for(nb, kBlock), kBlock, 0, st>>>(off64, 1, cursor, nb, pad_mask(td), fmt,
+                                                        tile_ent);
     DPS_LAUNCHED();
   }
   return bank_order(p16, nb, tile_off, tile_ent, st);
@@ -1325,9 +1331,10 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
   if (!tile_global(n_mids))
     return dps_ct_tiles_build(c_ptr, c_col, c_val, g, t_rank, n_targets, n_mids, tile_w, tile_off,
                               tile_ent, tile_maxc, tile_gmin, status_dev, ws, ws_bytes, stream);
-  const int shift = log2_exact(tile_w);
+  const TileDim td = tile_dim(tile_w);
+  const int shift = td.shift;
   DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED,
-              "tile_w must be a power of two in [256, 65536], got %d", tile_w);
+              "tile_w must be a power of two in [256, 65536], 7680 or 15360, got %d", tile_w);
   DPS_REQUIRE(n_targets >= 0 && n_mids >= 0 && nnz_cap >= 0, DPS_ERR_INVALID, "negative size");
   DPS_REQUIRE(n_targets < INT32_MAX && nnz_cap < UINT32_MAX, DPS_ERR_OVERFLOW,
               "n_targets / nnz capacity exceed 32 bits");
@@ -1382,10 +1389,10 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
     DPS_LAUNCHED();
     DPS_HIP_RET(scan_exclusive<uint32_t>(len, Q, n_targets, sws_q, scan_q, st));
     k_tile_keys<<<grid_for((n_targets + kWave - 1) / kWave * kWave, kBlock, 4096), kBlock, 0, st>>>(
-        c_ptr, c_col, c_val, t_rank, Q, n_targets, shift, cap, keys, vals, status_dev);
+        c_ptr, c_col, c_val, t_rank, Q, n_targets, td, cap, keys, vals, status_dev);
     DPS_LAUNCHED();
     if (tile_gmin) {
-      k_tile_gmin<<<static_cast<unsigned>(T), kBlock, 0, st>>>(perm, g, n_targets, shift, tile_gmin);
+      k_tile_gmin<<<static_cast<unsigned>(T), kBlock, 0, st>>>(perm, g, n_targets, td, tile_gmin);
       DPS_LAUNCHED();
     }
   }
@@ -1410,7 +1417,7 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
                                                            tile_off);
   DPS_LAUNCHED();
   k_sorted_write<<<grid_for(cap, kBlock), kBlock, 0, st>>>(keys_s, vals_s, cap, n_mids, T, fmt,
-                                                          static_cast<uint32_t>(tile_w) - 1u, P,
+                                                          pad_mask(td), P,
                                                           bstart, off64, tile_ent);
   DPS_LAUNCHED();
   return bank_order(fmt != kFmt32, nb, tile_off, tile_ent, st);
@@ -1421,8 +1428,8 @@ int dps_walk_row(const int32_t* src_col, const int32_t* src_val, int64_t src_len
                  const uint32_t* tile_off, const uint32_t* tile_ent, int64_t* out_m,
                  void* stream) {
   (void)n_mids;
-  const int shift = log2_exact(tile_w);
-  DPS_REQUIRE(shift >= 8 && shift <= 16, DPS_ERR_UNSUPPORTED, "bad tile_w %d", tile_w);
+  const TileDim td = tile_dim(tile_w);
+  DPS_REQUIRE(td.shift >= 8 && td.shift <= 16, DPS_ERR_UNSUPPORTED, "bad tile_w %d", tile_w);
   DPS_REQUIRE(src_len >= 0 && n_targets >= 0, DPS_ERR_INVALID, "negative size");
   auto st = static_cast<hipStream_t>(stream);
   const int64_t T = (n_targets + tile_w - 1) / tile_w;
@@ -1433,7 +1440,7 @@ int dps_walk_row(const int32_t* src_col, const int32_t* src_val, int64_t src_len
                                                    sizeof(int32_t))));
   k_walk_row<<<static_cast<unsigned>(T), kBlock,
                static_cast<size_t>(tile_w < 32768 ? tile_w : 32768) * sizeof(int32_t),
-               st>>>(src_col, src_val, src_len, n_targets, shift, T, tile_off, tile_ent, t_perm,
+               st>>>(src_col, src_val, src_len, n_targets, td, T, tile_off, tile_ent, t_perm,
                      out_m);
   DPS_LAUNCHED();
   return DPS_OK;

@@ -27,7 +27,7 @@ R_OTHER, R_AP, R_PX = 0, 1, 2
 STAT_MAX_C, STAT_MAX_DIAG, STAT_MAX_G, STAT_NNZ_C = 0, 1, 2, 3
 STATS_LEN = 8
 
-TUNE_WAVES_PER_ROW, TUNE_TILE_BUILD, TUNE_BANK_ORDER = 1, 2, 3
+TUNE_WAVES_PER_ROW, TUNE_TILE_BUILD, TUNE_BANK_ORDER, TUNE_LEAN_WPC = 1, 2, 3, 4
 
 
 class CctExt(C.Structure):

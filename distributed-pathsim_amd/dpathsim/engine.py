@@ -33,8 +33,17 @@ DEFAULT_HEAVY_VENUES = 32   # venue skipping: heavy venues in the dense table (6
 # venue skipping is exact; on config3 it scatters 41 % fewer chunks: at tile_w
 # 16384 the hot kernel takes 74.1 against 77.9 ms (profiles/r03/d), at 8192
 # 89.4 against 86.9 ms (profiles/r03/a) -- on by default for 16384 only
-VENUE_SKIP_TILE_W = (16384,)
+VENUE_SKIP_TILE_W = (16384, 15360)
 SYM_TILE_W = (8192, 16384)
+# the T15 layout (dps_cct1.hip Geo, round 6): 15 / 16 of 8192 / 16384 targets per
+# tile, so a wave's accumulator is 7680 bytes and 20 one-wave workgroups stay
+# resident per CU (8 KiB keeps 18: the CU's LDS is ~150 KiB in 512-byte granules)
+T15_TILE_W = (7680, 15360)
+FOUR_BIT_TILE_W = (16384, 15360)   # 4-bit counters, companion u8 halves at tile_w / 2
+
+
+def valid_tile_w(w: int) -> bool:
+    return w in T15_TILE_W or (not w & (w - 1) and 256 <= w <= 65536)
 DEFAULT_SYM_BAND = 1          # tiles either side of a row's own scanned by both rows
 DEFAULT_SYM_REC_PER_ROW = 32  # record capacity per row (config3: about 5 per row needed)
 
@@ -96,8 +105,8 @@ class PathSimEngine:
         if tile_w is None:
             self.bounds = host_bounds(typed)
             tile_w = auto_tile_w(typed, self.bounds)
-        if tile_w & (tile_w - 1) or not 256 <= tile_w <= 65536:
-            raise ValueError("tile_w must be a power of two in [256, 65536]")
+        if not valid_tile_w(int(tile_w)):
+            raise ValueError("tile_w must be a power of two in [256, 65536], 7680 or 15360")
         if denominator not in DENOMINATORS:
             raise ValueError(f"denominator must be one of {DENOMINATORS}")
         self.tile_w = int(tile_w)
@@ -108,7 +117,7 @@ class PathSimEngine:
         # venue skipping (dps_venue_skip): exact, row-sum denominator only
         self.venue_skip = tile_w in VENUE_SKIP_TILE_W and denominator == "rowsum"
         self.n_heavy = DEFAULT_HEAVY_VENUES
-        # tile_w 16384: the companion 8192-target u8 tiles for wide tiles
+        # 4-bit tiles (16384 / 15360): the companion u8 tiles of half the width
         self.half_tiles = True
         # ... and optimistic 4-bit passes over tiles whose bound is 16..255
         # (dps_cct_ext.tile_sum; exact either way, fewer passes)
@@ -320,32 +329,33 @@ class PathSimEngine:
                 del tws
             mark("tiles")
             half = None
-            if self.tile_w == 16384 and self.half_tiles:
-                # companion u8 tiles at 8192: a tile whose 4-bit bound exceeds 15
-                # runs as its two halves from these (dps_cct_ext)
-                T8 = max(1, math.ceil(NA / 8192)) if NA else 1
-                h_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV, NA, 8192)
+            if self.tile_w in FOUR_BIT_TILE_W and self.half_tiles:
+                # companion u8 tiles at half the width: a tile whose 4-bit bound
+                # exceeds 15 runs as its two halves from these (dps_cct_ext)
+                HW = self.tile_w // 2
+                T8 = max(1, math.ceil(NA / HW)) if NA else 1
+                h_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV, NA, HW)
                 if split:
-                    h_off, h_ent, h_maxc, _, h_status = self._split_tiles(split, sub, 8192, g_t,
+                    h_off, h_ent, h_maxc, _, h_status = self._split_tiles(split, sub, HW, g_t,
                                                                           False, h_cap)
                 else:
                     h_off = self._empty(NV * T8 + 1, torch.int32)
                     h_maxc = self._empty(NV * T8 + 1, torch.int32)
                     h_ent = self._empty(h_cap, torch.int32)
                     h_status = self._empty(1, torch.int32)
-                    hws = self._ws(_lib.size("dps_ct_tiles_workspace_size2", NV, NA, 8192,
+                    hws = self._ws(_lib.size("dps_ct_tiles_workspace_size2", NV, NA, HW,
                                              bnd.expand))
                     _lib.call("dps_ct_tiles_build2", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), None,
-                              _ptr(t_rank), NA, NV, 8192, bnd.expand, _ptr(h_off), _ptr(h_ent),
+                              _ptr(t_rank), NA, NV, HW, bnd.expand, _ptr(h_off), _ptr(h_ent),
                               _ptr(h_maxc), None, _ptr(h_status), _ptr(hws), hws.numel(), st)
                     del hws
                 # per-bucket count sums of the companion tiles: the hot kernel's
                 # optimistic 4-bit passes check each half's digit sum against
                 # them (dps_cct_ext.tile_sum)
                 t_sum = None
-                if self.opt_passes:
+                if self.opt_passes and self.tile_w not in T15_TILE_W:
                     t_sum = self._empty(NV * T8, torch.int32)
-                    _lib.call("dps_ct_tiles_sums", _ptr(h_off), _ptr(h_ent), NV * T8, 8192,
+                    _lib.call("dps_ct_tiles_sums", _ptr(h_off), _ptr(h_ent), NV * T8, HW,
                               _ptr(t_sum), st)
                 half = (h_off, h_ent, h_maxc, h_status, t_sum)
                 mark("half_tiles")

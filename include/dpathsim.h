@@ -80,10 +80,13 @@ const char* dps_last_error(void);
  *                           (automatic: by the number of mids);
  *   DPS_TUNE_BANK_ORDER     1 = order each C^T bucket's 16-bit entries for the
  *                           hot kernel's LDS banks, 2 = keep the build order
- *                           (automatic: see dps_ct_tiles_build).
+ *                           (automatic: see dps_ct_tiles_build);
+ *   DPS_TUNE_LEAN_WPC       1..32 one-wave workgroups per CU in the grid of the
+ *                           hot kernel's lean form (automatic: as many as its
+ *                           LDS and registers keep resident at once).
  * No reference counterpart (Spark picks its own plans). */
 enum { DPS_TUNE_WAVES_PER_ROW = 1, DPS_TUNE_TILE_BUILD = 2, DPS_TUNE_BANK_ORDER = 3,
-       DPS_TUNE_KEYS = 4 };
+       DPS_TUNE_LEAN_WPC = 4, DPS_TUNE_KEYS = 5 };
 int dps_set_tuning(int32_t key, int32_t value);
 int dps_get_tuning(int32_t key);
 /* Number of visible HIP devices (hipGetDeviceCount); < 0 on error. */

@@ -48,7 +48,7 @@ def decode_tiles(off, ent, n_mids, n_targets, tile_w):
     if tile_w <= 8192:                       # (l << 3) | e; e = 6, 7 at l % 4 == 3 pad
         l, e = h >> 3, h & 7
         pad = ((l & 3) == 3) & (e >= 6)
-    else:                                    # 16384: (l << 2) | e; e = 2, 3 at l % 8 == 7 pad
+    else:                                    # 16384 / 15360: (l << 2) | e; e = 2, 3 at l % 8 == 7 pad
         l, e = h >> 2, h & 3
         pad = ((l & 7) == 7) & (e >= 2)
     keep = ~pad
@@ -56,7 +56,7 @@ def decode_tiles(off, ent, n_mids, n_targets, tile_w):
     return b // T, (b % T) * tile_w + l[keep], np.left_shift(1, e[keep])
 
 
-@pytest.mark.parametrize("tile_w", [8192, 16384, 32768])
+@pytest.mark.parametrize("tile_w", [8192, 16384, 32768, 7680, 15360])
 def test_tile_format_decodes_to_c(tile_w):
     """Every C^T bucket decoded per the header sums to C[y, v] of the oracle
     (y = t_perm[label]), tile_maxc is the bucket maximum, tile_gmin the tile's
@@ -73,8 +73,8 @@ def test_tile_format_decodes_to_c(tile_w):
     want[row, cc[: cp[-1]]] = cv[: cp[-1]]
     perm = eng.tensor("t_perm")[:NA].cpu().numpy().astype(np.int64)
     sets = [(tile_w, "tile_off", "tile_ent", "tile_maxc")]
-    if tile_w == 16384:
-        sets.append((8192, "half_off", "half_ent", "half_maxc"))
+    if tile_w in (16384, 15360):
+        sets.append((tile_w // 2, "half_off", "half_ent", "half_maxc"))
     for w, o_n, e_n, m_n in sets:
         off = eng.tensor(o_n).cpu().numpy().view(np.uint32)
         ent = eng.tensor(e_n).cpu().numpy().view(np.uint32)

@@ -14,7 +14,8 @@ def _counts(eng):
 
 
 @pytest.mark.parametrize("tile_w,half,npass", [(8192, False, 4), (16384, False, 8),
-                                               (16384, True, 4)])
+                                               (16384, True, 4), (7680, False, 4),
+                                               (15360, False, 8), (15360, True, 4)])
 def test_lean_counters_without_tile_skipping(tile_w, half, npass):
     """With tile skipping off every tile of every row is scanned with 32-bit
     counters: 4 passes of 2048 targets per 8192-target tile (W = 8192, and W =
@@ -30,7 +31,7 @@ def test_lean_counters_without_tile_skipping(tile_w, half, npass):
     eng.venue_skip = False          # every bucket of the row's venues is scattered
     eng.upload().build()
     na, nv = t.n_authors, t.n_mids
-    tw = 8192 if half else tile_w
+    tw = tile_w // 2 if half else tile_w   # (the T15 widths 7680 / 15360 alike)
     T = (na + tw - 1) // tw
     cp = eng.tensor("c_ptr")[: na + 1].cpu().numpy()
     cc = eng.tensor("c_col")[: cp[-1]].cpu().numpy().astype(np.int64)

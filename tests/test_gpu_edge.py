@@ -197,7 +197,7 @@ def test_spgemm_long_and_huge_rows(multi, spgemm):
     _same([a.cpu().numpy() for a in eng.topk(10)], co.topk(10, 0, na))
 
 
-@pytest.mark.parametrize("tile_w", [8192, 16384])
+@pytest.mark.parametrize("tile_w", [8192, 16384, 7680, 15360])
 @pytest.mark.parametrize("k", [10, 100])
 def test_split_rows_identical_lean(tile_w, k):
     """The lean one-wave kernel's split path (the production shape): pieces of

@@ -196,7 +196,7 @@ def _crafted_wide_counts(n_fill=20000, seed=5):
                  ["author_of", "submit_at"], node_ids=lambda i: f"n{i}", labels=lambda i: f"L{i}")
 
 
-@pytest.mark.parametrize("tile_w", [8192, 16384])
+@pytest.mark.parametrize("tile_w", [8192, 16384, 7680, 15360])
 @pytest.mark.parametrize("k", [10, 100])
 def test_crafted_wide_passes(k, tile_w):
     import pathsim_oracle as po

@@ -26,7 +26,7 @@ def test_dblp_small_counts_bit_exact(small_engine, dblp_small_expected):
     assert np.array_equal(eng.tensor("g")[: len(ex["g"])].cpu().numpy(), ex["g"])
 
 
-@pytest.mark.parametrize("tile_w", [256, 512, 4096, 16384])
+@pytest.mark.parametrize("tile_w", [256, 512, 4096, 16384, 7680, 15360])
 def test_dblp_small_top10_bit_exact(dblp_small_tuples, dblp_small_expected, tile_w):
     from dpathsim.graph import Graph
     from dpathsim.engine import build_engine
@@ -63,7 +63,7 @@ def test_tile_skip_does_not_change_results(dblp_small_tuples, dblp_small_expecte
     assert np.array_equal(sc.cpu().numpy().view(np.int64), ex["top10_score"].view(np.int64))
 
 
-@pytest.mark.parametrize("tile_w", [256, 8192, 16384, 65536])
+@pytest.mark.parametrize("tile_w", [256, 8192, 16384, 65536, 7680, 15360])
 def test_single_source_walks_match_oracle(dblp_small_tuples, tile_w):
     """dps_walk_row / dps_pair_count / global walk; W = 65536 runs walk_row in
     two 32768-label parts."""

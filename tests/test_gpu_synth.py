@@ -23,7 +23,7 @@ def _check(eng, co, k, rows=None):
                            f"orc {oi[bad[0]]} {oc[bad[0]]} {os_[bad[0]]}")
 
 
-@pytest.mark.parametrize("tile_w", [256, 1024, 4096, 8192, 16384, 32768, 65536])
+@pytest.mark.parametrize("tile_w", [256, 1024, 4096, 8192, 16384, 32768, 65536, 7680, 15360])
 def test_synth_20k_top10(tile_w):
     from dpathsim.engine import build_engine
     from dpathsim.synth import synth_dblp

@@ -197,6 +197,14 @@ def test_c_abi_rejects_bad_arguments_without_gpu():
     rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 256, 8, 8, None, 8,
                           C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 512, None)
     assert rc == _lib.DPS_ERR_INVALID and b"16384" in lib.dps_last_error()
+    # the T15 widths (7680 / 15360) run without the optimistic passes' tile_sum
+    vs = _lib.CctExt(None, None, None, 0, 8, 8, 8, 8)
+    rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 15360, 8, 8, None, 8,
+                          C.addressof(vs), 0, 10, None, 10, 8, 8, 8, ws_al, 512, None)
+    assert rc == _lib.DPS_ERR_UNSUPPORTED and b"15360" in lib.dps_last_error()
+    rc = lib.dps_cct_topk(8, 8, 8, 8, None, None, None, 10, 5, 15000, 8, 8, None, 8,
+                          None, 0, 10, None, 10, 8, 8, 8, ws_al, 512, None)
+    assert rc == _lib.DPS_ERR_UNSUPPORTED and b"15360" in lib.dps_last_error()
     assert lib.dps_heavy_venues(None, 10, 0, None, None) == _lib.DPS_ERR_INVALID
     assert lib.dps_heavy_table(None, None, None, None, 10, None, 65, None, None) == _lib.DPS_ERR_INVALID
 
