@@ -951,7 +951,7 @@ size_t dps_cct_sym_workspace_size(int64_t n_targets, int32_t k, int64_t rec_cap)
   b += align_up(n * 4);                                          // rest-pass order
   b += 5 * align_up(cap * 4);                                    // records + placed records
   b += align_up(8) + 2 * align_up((n + 1) * 4) + align_up((n + 1) * 8);
-  b += align_up(scan_workspace_size(n_targets + 1)) + align_up(256);
+  b += align_up(scan_workspace_size(n_targets + 1)) + align_up(dps_cct_topk_workspace_size());
   return b + 1024;
 }
 
@@ -1004,7 +1004,9 @@ int dps_cct_sym(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val
   int64_t* off = c.take<int64_t>(n + 1);
   const size_t scan_ws = scan_workspace_size(n + 1);
   void* sws = c.take<char>(scan_ws);
-  unsigned long long* band_ctr = c.take<unsigned long long>(32);
+  // (the hot kernel's counter words, dps_cct_topk_workspace_size bytes)
+  unsigned long long* band_ctr =
+      c.take<unsigned long long>(dps_cct_topk_workspace_size() / sizeof(unsigned long long));
   DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "cct_sym workspace carve failed");
   {
     FillSet fs;
@@ -1023,7 +1025,8 @@ int dps_cct_sym(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val
   sy.sym = 1;
   int rc = cct_topk_impl(c_ptr, c_col, c_val, g, g_t, t_perm, t_rank, n, n_mids, tile_w, tile_off,
                          tile_ent, tile_maxc, tile_gmin, ext, 0, n, row_order, false, k, out_idx,
-                         out_cnt, out_score, band_ctr, 256, stream, 0, nullptr, nullptr, nullptr,
+                         out_cnt, out_score, band_ctr, dps_cct_topk_workspace_size(), stream, 0,
+                         nullptr, nullptr, nullptr,
                          nullptr, nullptr, &sy);
   if (rc != DPS_OK) return rc;
   // 2. plan: strong rows and the emission thresholds
