@@ -53,7 +53,7 @@ def parse():
                     help="1/0: force venue skipping on/off (default: the engine's)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r05", "pmc_hot.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r06", "pmc_hot.json"),
                     help="rocprofv3 PMC summary of the hot kernel at HEAD (tools/pmc_hot.py): "
                          "HBM bytes per launch (roofline.traffic) and VALU issue share")
     return ap.parse_args()
