@@ -82,13 +82,11 @@ constexpr uint32_t kLabMask1 = 0x1FFCu;       // (entry >> 3) & mask = dword byt
 template <int F> struct Fmt;
 template <> struct Fmt<1> {
   static constexpr int S = 13;                // log2 W
-  static constexpr int SEG = 10;              // threshold segments of 1024 targets
   static constexpr int BITS = 8;              // counter bits of the base pass
   static constexpr uint32_t UB0 = 0xFFu;      // largest bound of the base pass
 };
 template <> struct Fmt<2> {
   static constexpr int S = 14;
-  static constexpr int SEG = 11;              // 2048 targets: one 64-lane x 16 B block
   static constexpr int BITS = 4;
   static constexpr uint32_t UB0 = 0xFu;
 };

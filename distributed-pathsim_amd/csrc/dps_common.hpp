@@ -220,7 +220,7 @@ __device__ __forceinline__ int opaque_lane(int lane) {
 // ---- several dword ranges set in one launch (dps_scan.hip) ---------------------
 // Replaces a hipMemsetAsync per small array (each one a fill kernel of its own).
 struct FillSet {
-  static constexpr int kMax = 8;
+  static constexpr int kMax = 16;
   uint32_t* p[kMax];
   int64_t n[kMax];    // dwords
   uint32_t v[kMax];

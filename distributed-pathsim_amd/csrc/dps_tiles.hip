@@ -701,6 +701,152 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_blk(
 }
 
 // --------------------------------------------------------------------------
+// Both tile sets of the bench shape in one walk of C (round 6):
+// the 4-bit tiles A (16384 / 15360 targets) and their companion u8 half tiles
+// B (8192 / 7680).  A part (lpb labels) lies inside one tile of each set, so a
+// block stages its labels and walks its entries once and counts -- then places
+// -- every entry in both formats; the per-(venue, part) maximum is shared (the
+// same C values).  Count LDS: two count arrays and one maximum, 96 KiB + the
+// staged rows; scatter: two 32-bit cursor arrays (the host checks both sets'
+// entries fit 32 bits).
+__global__ __launch_bounds__(kBlkThreads) void k_tile_count_dual(
+    const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
+    const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm,
+    const int64_t* __restrict__ g, int64_t n_targets, int64_t n_mids, TileDim tdA, int64_t TA,
+    TileDim tdB, int64_t TB, int labels_per_block, int PA, int PB, int S, int n_ranges,
+    const uint32_t* __restrict__ part_n, uint32_t* __restrict__ cntpA, uint32_t* __restrict__ mxpA,
+    uint32_t* __restrict__ cntpB, uint32_t* __restrict__ mxpB,
+    unsigned long long* __restrict__ gmin, int32_t* __restrict__ status) {
+  __shared__ uint32_t cntA_s[kBlkMids];
+  __shared__ uint32_t cntB_s[kBlkMids];
+  __shared__ uint32_t mx_s[kBlkMids];
+  __shared__ uint32_t rel_s[kBlkLabels + 1];
+  __shared__ int64_t d_s[kBlkLabels];
+  __shared__ int tab_s[kMaxStrips + 1];
+  __shared__ uint32_t wsum[kBlkThreads / kWave];
+  __shared__ unsigned long long gmin_s;
+  __shared__ int ovf_s;
+  const int64_t n_parts = gridDim.x / (static_cast<int64_t>(S) * n_ranges);
+  const int64_t part = blockIdx.x % n_parts;
+  const int64_t q = blockIdx.x / n_parts;
+  const uint32_t sb = static_cast<uint32_t>(q % S);
+  const MidRange mr = mid_range(q / S, n_mids);
+  const SubRange sr = sub_range(part_n[part], sb, S);
+  if (static_cast<int>(sb) >= sr.n_sub) return;   // block-uniform: before any barrier
+  for (int v = threadIdx.x; v < mr.n; v += kBlkThreads) { cntA_s[v] = 0; cntB_s[v] = 0; mx_s[v] = 0; }
+  if (threadIdx.x == 0) { gmin_s = ~0ull; ovf_s = 0; }
+  const int fmtA = tile_fmt(tdA.shift), fmtB = tile_fmt(tdB.shift);
+  const int64_t l0 = part * labels_per_block;
+  const int64_t l1 = min(l0 + labels_per_block, n_targets);
+  const int64_t tA = tdA.tile(l0), tB = tdB.tile(l0);
+  const int64_t hA = part % PA, hB = part % PB;
+  __syncthreads();
+  const BlockRows R{rel_s, d_s};
+  const int nl = static_cast<int>(l1 - l0);
+  const bool do_g = gmin && sb == 0 && mr.m0 == 0;
+  stage_rows(c_ptr, perm, do_g ? g : nullptr, l0, l1, R, wsum, &gmin_s);
+  if (sr.e1 - sr.e0 <= kMaxStrips * kWave) strip_table(R, nl, sr.e0, sr.e1, tab_s);
+  const uint32_t lab0 = static_cast<uint32_t>(l0);   // (the pieces depend on label % 8 only)
+  walk_strips(R, nl, sr.e0, sr.e1, tab_s, c_col, c_val, [&](int i, int32_t v, int32_t c) {
+    if (c > 0xFFFF) ovf_s = 1;
+    const uint32_t lv = static_cast<uint32_t>(v - mr.m0);
+    if (lv >= static_cast<uint32_t>(mr.n)) return;
+    const uint32_t lab = lab0 + static_cast<uint32_t>(i);
+    atomicAdd(&cntA_s[lv], n_pieces(fmtA, static_cast<uint32_t>(c), lab));
+    atomicAdd(&cntB_s[lv], n_pieces(fmtB, static_cast<uint32_t>(c), lab));
+    if (c > 1) atomicMax(&mx_s[lv], static_cast<uint32_t>(c));
+  });
+  __syncthreads();
+  if (threadIdx.x == 0 && ovf_s && status) *status = DPS_ERR_OVERFLOW;
+  for (int lv = threadIdx.x; lv < mr.n; lv += kBlkThreads) {
+    if (!cntA_s[lv]) continue;
+    const int64_t v = mr.m0 + lv;
+    const int64_t sa = (v * TA + tA) * PA + hA, sbb = (v * TB + tB) * PB + hB;
+    if (sr.n_sub == 1) {
+      cntpA[sa] = cntA_s[lv];
+      mxpA[sa] = mx_s[lv];
+      cntpB[sbb] = cntB_s[lv];
+      mxpB[sbb] = mx_s[lv];
+    } else {
+      atomicAdd(&cntpA[sa], cntA_s[lv]);
+      atomicAdd(&cntpB[sbb], cntB_s[lv]);
+      if (mx_s[lv]) {
+        atomicMax(&mxpA[sa], mx_s[lv]);
+        atomicMax(&mxpB[sbb], mx_s[lv]);
+      }
+    }
+  }
+  if (threadIdx.x == 0 && do_g && gmin_s != ~0ull) atomicMin(&gmin[tA], gmin_s);
+}
+
+__global__ __launch_bounds__(kBlkThreads) void k_tile_scatter_dual(
+    const int64_t* __restrict__ c_ptr, const int32_t* __restrict__ c_col,
+    const int32_t* __restrict__ c_val, const int32_t* __restrict__ perm, int64_t n_targets,
+    int64_t n_mids, TileDim tdA, int64_t TA, TileDim tdB, int64_t TB, int labels_per_block, int PA,
+    int PB, int S, int n_ranges, const uint32_t* __restrict__ part_n,
+    const int64_t* __restrict__ offpA, uint32_t* __restrict__ curpA, uint32_t* __restrict__ entA,
+    const int64_t* __restrict__ offpB, uint32_t* __restrict__ curpB, uint32_t* __restrict__ entB) {
+  __shared__ uint32_t baseA_s[kBlkMids];   // counts, then 32-bit entry cursors
+  __shared__ uint32_t baseB_s[kBlkMids];
+  __shared__ uint32_t rel_s[kBlkLabels + 1];
+  __shared__ int64_t d_s[kBlkLabels];
+  __shared__ int tab_s[kMaxStrips + 1];
+  __shared__ uint32_t wsum[kBlkThreads / kWave];
+  const int64_t n_parts = gridDim.x / (static_cast<int64_t>(S) * n_ranges);
+  const int64_t part = blockIdx.x % n_parts;
+  const int64_t q = blockIdx.x / n_parts;
+  const uint32_t sb = static_cast<uint32_t>(q % S);
+  const MidRange mr = mid_range(q / S, n_mids);
+  const SubRange sr = sub_range(part_n[part], sb, S);
+  if (static_cast<int>(sb) >= sr.n_sub) return;   // block-uniform: before any barrier
+  for (int v = threadIdx.x; v < mr.n; v += kBlkThreads) { baseA_s[v] = 0; baseB_s[v] = 0; }
+  const int fmtA = tile_fmt(tdA.shift), fmtB = tile_fmt(tdB.shift);
+  const int64_t l0 = part * labels_per_block;
+  const int64_t l1 = min(l0 + labels_per_block, n_targets);
+  const int64_t tA = tdA.tile(l0), tB = tdB.tile(l0);
+  const int64_t hA = part % PA, hB = part % PB;
+  __syncthreads();
+  const BlockRows R{rel_s, d_s};
+  const int nl = static_cast<int>(l1 - l0);
+  stage_rows(c_ptr, perm, nullptr, l0, l1, R, wsum, nullptr);
+  if (sr.e1 - sr.e0 <= kMaxStrips * kWave) strip_table(R, nl, sr.e0, sr.e1, tab_s);
+  const uint32_t labA0 = tdA.local(l0), labB0 = tdB.local(l0);   // (a part lies in one tile)
+  if (sr.n_sub == 1) {
+    for (int lv = threadIdx.x; lv < mr.n; lv += kBlkThreads) {
+      baseA_s[lv] = static_cast<uint32_t>(offpA[((mr.m0 + lv) * TA + tA) * PA + hA]);
+      baseB_s[lv] = static_cast<uint32_t>(offpB[((mr.m0 + lv) * TB + tB) * PB + hB]);
+    }
+  } else {
+    walk_strips(R, nl, sr.e0, sr.e1, tab_s, c_col, c_val, [&](int i, int32_t v, int32_t c) {
+      const uint32_t lv = static_cast<uint32_t>(v - mr.m0);
+      if (lv >= static_cast<uint32_t>(mr.n)) return;
+      atomicAdd(&baseA_s[lv], n_pieces(fmtA, static_cast<uint32_t>(c), labA0 + static_cast<uint32_t>(i)));
+      atomicAdd(&baseB_s[lv], n_pieces(fmtB, static_cast<uint32_t>(c), labB0 + static_cast<uint32_t>(i)));
+    });
+    __syncthreads();
+    for (int lv = threadIdx.x; lv < mr.n; lv += kBlkThreads) {
+      const uint32_t na = baseA_s[lv];
+      if (!na) continue;
+      const int64_t sa = ((mr.m0 + lv) * TA + tA) * PA + hA;
+      const int64_t sbb = ((mr.m0 + lv) * TB + tB) * PB + hB;
+      baseA_s[lv] = static_cast<uint32_t>(offpA[sa] + atomicAdd(&curpA[sa], na));
+      baseB_s[lv] = static_cast<uint32_t>(offpB[sbb] + atomicAdd(&curpB[sbb], baseB_s[lv]));
+    }
+  }
+  __syncthreads();
+  walk_strips(R, nl, sr.e0, sr.e1, tab_s, c_col, c_val, [&](int i, int32_t v, int32_t c) {
+    const uint32_t lv = static_cast<uint32_t>(v - mr.m0);
+    if (lv >= static_cast<uint32_t>(mr.n)) return;
+    const uint32_t cu = static_cast<uint32_t>(c);
+    const uint32_t la = labA0 + static_cast<uint32_t>(i), lb = labB0 + static_cast<uint32_t>(i);
+    const uint32_t pa = atomicAdd(&baseA_s[lv], n_pieces(fmtA, cu, la));
+    put_entry(fmtA, entA, static_cast<int64_t>(pa), cu, la);
+    const uint32_t pb = atomicAdd(&baseB_s[lv], n_pieces(fmtB, cu, lb));
+    put_entry(fmtB, entB, static_cast<int64_t>(pb), cu, lb);
+  });
+}
+
+// --------------------------------------------------------------------------
 // Single-source dense row: one block per target tile; out_m in ORIGINAL order.
 __global__ __launch_bounds__(kBlock) void k_walk_row(const int32_t* __restrict__ src_col,
                                                      const int32_t* __restrict__ src_val,
@@ -1421,6 +1567,160 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
                                                           bstart, off64, tile_ent);
   DPS_LAUNCHED();
   return bank_order(fmt != kFmt32, nb, tile_off, tile_ent, st);
+}
+
+size_t dps_ct_tiles_workspace_size_dual(int64_t n_mids, int64_t n_targets, int32_t tile_w,
+                                        int64_t nnz_cap) {
+  const TileDim tdA = tile_dim(tile_w);
+  if (tdA.shift != 14 || tile_w <= 0) return 0;
+  const int32_t hw = tile_w / 2;
+  const size_t a2 = dps_ct_tiles_workspace_size2(n_mids, n_targets, tile_w, nnz_cap);
+  const size_t b2 = dps_ct_tiles_workspace_size2(n_mids, n_targets, hw, nnz_cap);
+  const size_t fb = a2 > b2 ? a2 : b2;                 // the two-call path
+  if (tile_global(n_mids)) return fb;
+  const int64_t TA = (n_targets + tile_w - 1) / tile_w, TB = (n_targets + hw - 1) / hw;
+  const int64_t nbA = n_mids * (TA > 0 ? TA : 1), nbB = n_mids * (TB > 0 ? TB : 1);
+  const int lpb = tile_lpb(tile_w);
+  const int64_t npA = nbA * (tile_w / lpb), npB = nbB * (hw / lpb);
+  const int64_t nblk = (n_targets + lpb - 1) / lpb;
+  size_t s = 0;
+  s += align_up(static_cast<size_t>(nbA + 1) * 4) + align_up(static_cast<size_t>(nbB + 1) * 4);
+  s += align_up(static_cast<size_t>(npA + 1) * 8) + align_up(static_cast<size_t>(npB + 1) * 8);
+  s += align_up(scan_workspace_size((npA > npB ? npA : npB) + 1));
+  s += 3 * align_up(static_cast<size_t>(npA + 1) * 4) + 3 * align_up(static_cast<size_t>(npB + 1) * 4);
+  s += align_up(static_cast<size_t>(nblk + 1) * 4);
+  s += align_up(static_cast<size_t>(n_targets > 0 ? n_targets : 1) * 4);
+  s += 1024;
+  return s > fb ? s : fb;
+}
+
+int dps_ct_tiles_build_dual(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                            const int64_t* g, const int32_t* t_rank, int64_t n_targets,
+                            int64_t n_mids, int32_t tile_w, int64_t nnz_cap, uint32_t* tile_off,
+                            uint32_t* tile_ent, int64_t tile_ent_words, uint32_t* tile_maxc,
+                            int64_t* tile_gmin, uint32_t* half_off, uint32_t* half_ent,
+                            int64_t half_ent_words, uint32_t* half_maxc, int32_t* status_dev,
+                            int32_t* half_status, void* ws, size_t ws_bytes, void* stream) {
+  const TileDim tdA = tile_dim(tile_w), tdB = tile_dim(tile_w / 2);
+  DPS_REQUIRE(tdA.shift == 14 && tdB.shift == 13 && tdA.t15 == tdB.t15, DPS_ERR_UNSUPPORTED,
+              "the dual build takes tile_w 16384 or 15360 (4-bit tiles), got %d", tile_w);
+  DPS_REQUIRE(n_targets >= 0 && n_mids >= 0 && nnz_cap >= 0, DPS_ERR_INVALID, "negative size");
+  DPS_REQUIRE(n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "n_targets exceeds int32");
+  DPS_REQUIRE(!tile_gmin || g, DPS_ERR_INVALID, "tile_gmin needs g");
+  DPS_REQUIRE(tile_off && tile_ent && half_off && half_ent, DPS_ERR_INVALID, "null tile arrays");
+  DPS_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 256 == 0, DPS_ERR_WORKSPACE,
+              "workspace not 256-byte aligned");
+  DPS_REQUIRE(ws_bytes >= dps_ct_tiles_workspace_size_dual(n_mids, n_targets, tile_w, nnz_cap),
+              DPS_ERR_WORKSPACE, "tiles workspace too small");
+  const int32_t hw = tile_w / 2;
+  // many mids, or 16-bit entry offsets beyond the scatter's 32-bit cursors:
+  // the two builds one after the other (they reuse the workspace)
+  if (tile_global(n_mids) || 2 * tile_ent_words >= (int64_t(1) << 32) ||
+      2 * half_ent_words >= (int64_t(1) << 32)) {
+    const int rc = dps_ct_tiles_build2(c_ptr, c_col, c_val, g, t_rank, n_targets, n_mids, tile_w,
+                                       nnz_cap, tile_off, tile_ent, tile_maxc, tile_gmin,
+                                       status_dev, ws, ws_bytes, stream);
+    if (rc != DPS_OK) return rc;
+    return dps_ct_tiles_build2(c_ptr, c_col, c_val, nullptr, t_rank, n_targets, n_mids, hw,
+                               nnz_cap, half_off, half_ent, half_maxc, nullptr, half_status, ws,
+                               ws_bytes, stream);
+  }
+  auto st = static_cast<hipStream_t>(stream);
+  const int64_t TA = (n_targets + tile_w - 1) / tile_w, TB = (n_targets + hw - 1) / hw;
+  const int64_t nbA = n_mids * TA, nbB = n_mids * TB;
+  const int n_ranges = static_cast<int>(n_mids > 0 ? (n_mids + kBlkMids - 1) / kBlkMids : 1);
+  const int lpb = tile_lpb(tile_w);
+  const int PA = tile_w / lpb, PB = hw / lpb;
+  const int64_t npA = nbA * PA, npB = nbB * PB;
+  const int64_t nblk = (n_targets + lpb - 1) / lpb;
+  const int S = tile_sub();
+  DPS_REQUIRE(nblk * S * n_ranges < INT32_MAX, DPS_ERR_OVERFLOW, "too many tile-build blocks");
+  Carve c(ws, ws_bytes);
+  uint32_t* cntA = c.take<uint32_t>(nbA + 1);
+  uint32_t* cntB = c.take<uint32_t>(nbB + 1);
+  int64_t* offA = c.take<int64_t>(npA + 1);
+  int64_t* offB = c.take<int64_t>(npB + 1);
+  const size_t scan_ws = scan_workspace_size((npA > npB ? npA : npB) + 1);
+  void* sws = c.take<char>(scan_ws);
+  uint32_t* cntpA = c.take<uint32_t>(npA + 1);
+  uint32_t* mxpA = c.take<uint32_t>(npA + 1);
+  uint32_t* curpA = c.take<uint32_t>(npA + 1);
+  uint32_t* cntpB = c.take<uint32_t>(npB + 1);
+  uint32_t* mxpB = c.take<uint32_t>(npB + 1);
+  uint32_t* curpB = c.take<uint32_t>(npB + 1);
+  uint32_t* part_n = c.take<uint32_t>(nblk + 1);
+  int32_t* perm = c.take<int32_t>(n_targets > 0 ? n_targets : 1);
+  DPS_REQUIRE(c.ok, DPS_ERR_WORKSPACE, "tiles workspace carve failed");
+  {
+    FillSet fs;   // every counter, both status words and the tile minima in one launch
+    fs.add(part_n, nblk + 1, 0u);
+    fs.add(cntpA, npA + 1, 0u);
+    fs.add(mxpA, npA + 1, 0u);
+    fs.add(curpA, npA + 1, 0u);
+    fs.add(cntpB, npB + 1, 0u);
+    fs.add(mxpB, npB + 1, 0u);
+    fs.add(curpB, npB + 1, 0u);
+    if (status_dev) fs.add(status_dev, 1, 0u);
+    if (half_status) fs.add(half_status, 1, 0u);
+    if (tile_gmin && TA > 0) fs.add(tile_gmin, 2 * TA, 0x7F7F7F7Fu);
+    if (tile_maxc) fs.add(tile_maxc + nbA, 1, 0u);
+    if (half_maxc) fs.add(half_maxc + nbB, 1, 0u);
+    DPS_HIP_RET(fill_set(fs, st));
+  }
+  if (n_targets > 0 && nblk <= kPartLds) {
+    k_invert_and_parts<<<grid_for(n_targets, kBlock, 1024), kBlock, 0, st>>>(
+        t_rank, c_ptr, n_targets, lpb, static_cast<int>(nblk), perm, part_n);
+    DPS_LAUNCHED();
+  } else if (n_targets > 0) {
+    if (t_rank) {
+      k_tile_invert<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(t_rank, n_targets, perm);
+      DPS_LAUNCHED();
+    }
+    k_part_entries<<<grid_for(n_targets, kBlock), kBlock, 0, st>>>(c_ptr, t_rank ? perm : nullptr,
+                                                                   n_targets, lpb, part_n);
+    DPS_LAUNCHED();
+  }
+  const int32_t* perm_or_null = t_rank ? perm : nullptr;
+  const int fmtA = tile_fmt(tdA.shift), fmtB = tile_fmt(tdB.shift);
+  const unsigned grid = static_cast<unsigned>(nblk * S * n_ranges);
+  if (n_targets > 0 && nbA > 0) {
+    k_tile_count_dual<<<grid, kBlkThreads, 0, st>>>(
+        c_ptr, c_col, c_val, perm_or_null, tile_gmin ? g : nullptr, n_targets, n_mids, tdA, TA, tdB,
+        TB, lpb, PA, PB, S, n_ranges, part_n, cntpA, mxpA, cntpB, mxpB,
+        reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
+    DPS_LAUNCHED();
+  }
+  if (nbA > 0) {
+    k_tile_parts_fix<<<grid_for(nbA, kBlock), kBlock, 0, st>>>(cntpA, mxpA, nbA, PA, 8u, cntA,
+                                                                tile_maxc);
+    DPS_LAUNCHED();
+    k_tile_parts_fix<<<grid_for(nbB, kBlock), kBlock, 0, st>>>(cntpB, mxpB, nbB, PB, 8u, cntB,
+                                                                half_maxc);
+    DPS_LAUNCHED();
+  }
+  DPS_HIP_RET(scan_exclusive<uint32_t>(cntpA, offA, npA, sws, scan_ws, st));
+  k_tile_off32<<<grid_for(nbA + 1, kBlock), kBlock, 0, st>>>(offA, PA, nbA, 1, tile_off);
+  DPS_LAUNCHED();
+  DPS_HIP_RET(scan_exclusive<uint32_t>(cntpB, offB, npB, sws, scan_ws, st));
+  k_tile_off32<<<grid_for(nbB + 1, kBlock), kBlock, 0, st>>>(offB, PB, nbB, 1, half_off);
+  DPS_LAUNCHED();
+  if (n_targets > 0 && nbA > 0) {
+    k_tile_scatter_dual<<<grid, kBlkThreads, 0, st>>>(
+        c_ptr, c_col, c_val, perm_or_null, n_targets, n_mids, tdA, TA, tdB, TB, lpb, PA, PB, S,
+        n_ranges, part_n, offA, curpA, tile_ent, offB, curpB, half_ent);
+    DPS_LAUNCHED();
+  }
+  if (nbA > 0) {
+    k_tile_pad<<<grid_for(nbA, kBlock), kBlock, 0, st>>>(offA, PA, cntA, nbA, pad_mask(tdA), fmtA,
+                                                         tile_ent);
+    DPS_LAUNCHED();
+    k_tile_pad<<<grid_for(nbB, kBlock), kBlock, 0, st>>>(offB, PB, cntB, nbB, pad_mask(tdB), fmtB,
+                                                         half_ent);
+    DPS_LAUNCHED();
+  }
+  const int rc = bank_order(true, nbA, tile_off, tile_ent, st);
+  if (rc != DPS_OK) return rc;
+  return bank_order(true, nbB, half_off, half_ent, st);
 }
 
 int dps_walk_row(const int32_t* src_col, const int32_t* src_val, int64_t src_len,

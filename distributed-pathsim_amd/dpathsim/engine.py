@@ -119,6 +119,8 @@ class PathSimEngine:
         self.n_heavy = DEFAULT_HEAVY_VENUES
         # 4-bit tiles (16384 / 15360): the companion u8 tiles of half the width
         self.half_tiles = True
+        # ... built together with the 4-bit tiles in one walk of C (round 6)
+        self.dual_build = True
         # ... and optimistic 4-bit passes over tiles whose bound is 16..255
         # (dps_cct_ext.tile_sum; exact either way, fewer passes)
         self.opt_passes = False   # round 4: measured, see DESIGN §6 (off until it wins)
@@ -309,9 +311,41 @@ class PathSimEngine:
             if ent_cap >= 2 ** 32:
                 raise OverflowError("padded nnz(C) >= 2^32 exceeds the uint32 tile offsets")
             sub = self._label_rows(split, c_ptr, c_col, c_val, t_perm) if split else None
+            # the 4-bit tiles and their companion u8 halves from one walk of C
+            # (dps_ct_tiles_build_dual) -- replicated builds only
+            dual = (not split and self.dual_build and self.half_tiles
+                    and self.tile_w in FOUR_BIT_TILE_W)
+            half = None
             if split:
                 tile_off, tile_ent, tile_maxc, tile_gmin, status = self._split_tiles(
                     split, sub, self.tile_w, g_t, True, ent_cap)
+            elif dual:
+                HW = self.tile_w // 2
+                T8 = max(1, math.ceil(NA / HW)) if NA else 1
+                h_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV, NA, HW)
+                tile_off = self._empty(NV * T + 1, torch.int32)
+                tile_maxc = self._empty(NV * T + 1, torch.int32)
+                tile_gmin = self._empty(T, torch.int64)
+                tile_ent = self._empty(ent_cap, torch.int32)
+                status = self._empty(1, torch.int32)
+                h_off = self._empty(NV * T8 + 1, torch.int32)
+                h_maxc = self._empty(NV * T8 + 1, torch.int32)
+                h_ent = self._empty(h_cap, torch.int32)
+                h_status = self._empty(1, torch.int32)
+                tws = self._ws(_lib.size("dps_ct_tiles_workspace_size_dual", NV, NA, self.tile_w,
+                                         bnd.expand))
+                _lib.call("dps_ct_tiles_build_dual", _ptr(c_ptr), _ptr(c_col), _ptr(c_val),
+                          _ptr(den), _ptr(t_rank), NA, NV, self.tile_w, bnd.expand, _ptr(tile_off),
+                          _ptr(tile_ent), tile_ent.numel(), _ptr(tile_maxc), _ptr(tile_gmin),
+                          _ptr(h_off), _ptr(h_ent), h_ent.numel(), _ptr(h_maxc), _ptr(status),
+                          _ptr(h_status), _ptr(tws), tws.numel(), st)
+                del tws
+                t_sum = None            # (the optimistic passes' sums, as below)
+                if self.opt_passes and self.tile_w not in T15_TILE_W:
+                    t_sum = self._empty(NV * T8, torch.int32)
+                    _lib.call("dps_ct_tiles_sums", _ptr(h_off), _ptr(h_ent), NV * T8, HW,
+                              _ptr(t_sum), st)
+                half = (h_off, h_ent, h_maxc, h_status, t_sum)
             else:
                 tile_off = self._empty(NV * T + 1, torch.int32)
                 tile_maxc = self._empty(NV * T + 1, torch.int32)
@@ -328,8 +362,7 @@ class PathSimEngine:
                           tws.numel(), st)
                 del tws
             mark("tiles")
-            half = None
-            if self.tile_w in FOUR_BIT_TILE_W and self.half_tiles:
+            if not dual and self.tile_w in FOUR_BIT_TILE_W and self.half_tiles:
                 # companion u8 tiles at half the width: a tile whose 4-bit bound
                 # exceeds 15 runs as its two halves from these (dps_cct_ext)
                 HW = self.tile_w // 2

@@ -267,18 +267,20 @@ int dps_target_order(const int64_t* g, int64_t n_targets, int32_t key_bits,
 /* ---------------------------------------------------------------------------
  * A5 operand layout, step 2: target-tiled transpose of C for the C.C^T kernels.
  * Target labels (t_rank[y], or y if t_rank == NULL) in [0, n_targets) are cut
- * into tiles of `tile_w` (power of two, 256..65536; the hot kernel keeps one
- * tile's packed counters in LDS: u8 at tile_w 8192, 4-bit at 16384).  Bucket
+ * into tiles of `tile_w` (a power of two, 256..65536, or the T15 widths 7680 /
+ * 15360; the hot kernel keeps one tile's packed counters in LDS: u8 at tile_w
+ * 8192 / 7680, 4-bit at 16384 / 15360 -- the T15 widths take 7680 bytes, so 20
+ * one-wave workgroups stay resident per CU instead of 18).  Bucket
  * (v, t) holds, for every y of tile t with C[y,v] > 0, packed entries in one of
  * three formats, l = label(y) - t*tile_w:
- *   tile_w <= 8192:  uint16 (l << 3) | e, one piece of value 2^e: C[y,v] is
+ *   tile_w <= 8192 (and 7680):  uint16 (l << 3) | e, one piece of value 2^e: C[y,v] is
  *                    split into power-of-two pieces that sum to it (as many
  *                    2^emax as fit, then the set bits of the rest), emax = 7,
  *                    or 5 when l % 4 == 3 (e = 6, 7 at l % 4 == 3 are padding
  *                    codes).  The low five bits 8*(l % 4) + e are the shift
  *                    that adds C[x,v]*2^e to target l's byte of a packed-u8
  *                    dword;
- *   tile_w == 16384: uint16 (l << 2) | e, the same for packed 4-bit counters:
+ *   tile_w 16384 / 15360: uint16 (l << 2) | e, the same for packed 4-bit counters:
  *                    emax = 3, or 1 when l % 8 == 7 (e = 2, 3 at l % 8 == 7 are
  *                    padding codes); low five bits 4*(l % 8) + e;
  *   tile_w >= 32768: uint32 (C[y,v] << 16) | l, one entry per (y, v).
@@ -315,6 +317,26 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
                         int32_t tile_w, int64_t nnz_cap, uint32_t* tile_off, uint32_t* tile_ent,
                         uint32_t* tile_maxc, int64_t* tile_gmin, int32_t* status_dev, void* ws,
                         size_t ws_bytes, void* stream);
+/* Both tile sets the bench shape's hot kernel reads, from one walk of C (round
+ * 6): the 4-bit tiles at tile_w (16384 or 15360: tile_off / tile_ent /
+ * tile_maxc / tile_gmin) and their companion u8 tiles at tile_w / 2 (half_off /
+ * half_ent / half_maxc, no minima) -- bit for bit the outputs of two
+ * dps_ct_tiles_build2 calls (offsets and maxima; entries as multisets per
+ * bucket), which it makes itself with many mids (more than 8 * 8192) or when
+ * the entry buffers' sizes (tile_ent_words / half_ent_words, uint32 words) reach
+ * 2^31.  Overflow (max C > 65535) goes to *status_dev; *half_status is zeroed
+ * (and set only by the two-call path).  ws: dps_ct_tiles_workspace_size_dual
+ * (0 for other widths).  Replaces nothing in the reference (layout only); A5's
+ * operand build, DPathSim_APVPA.py:90-109. */
+size_t dps_ct_tiles_workspace_size_dual(int64_t n_mids, int64_t n_targets, int32_t tile_w,
+                                        int64_t nnz_cap);
+int dps_ct_tiles_build_dual(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
+                            const int64_t* g, const int32_t* t_rank, int64_t n_targets,
+                            int64_t n_mids, int32_t tile_w, int64_t nnz_cap, uint32_t* tile_off,
+                            uint32_t* tile_ent, int64_t tile_ent_words, uint32_t* tile_maxc,
+                            int64_t* tile_gmin, uint32_t* half_off, uint32_t* half_ent,
+                            int64_t half_ent_words, uint32_t* half_maxc, int32_t* status_dev,
+                            int32_t* half_status, void* ws, size_t ws_bytes, void* stream);
 /* Per-bucket count sums of built tiles: tile_sum[b] = sum over the bucket's
  * entries of their values (2^e of a 16-bit piece, padding codes excluded; C of
  * a 32-bit entry) = sum_{y of tile t} C[y,v] for bucket b = v*T + t, b <

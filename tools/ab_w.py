@@ -32,6 +32,7 @@ for W, NW in cases:
         # optimistic 4-bit passes (engine.opt_passes, dps_cct_ext.tile_sum): on in
         # A/B runs only with AB_OPT=1 (the engine default is off)
         eng.opt_passes = os.environ.get("AB_OPT", "0") == "1"
+        eng.dual_build = os.environ.get("AB_DUAL", "1") == "1"   # one-walk tile build (round 6)
         if os.environ.get("AB_SPLIT"):      # "rows:pieces" of the heavy-row split
             eng.split_rows, eng.pieces = (int(v) for v in os.environ["AB_SPLIT"].split(":"))
         eng.upload().build()
