@@ -103,7 +103,10 @@ def main():
                 except Exception as e:    # noqa: BLE001 -- falls back below, on every rank
                     print(f"rank {rank}: dps_comm_init failed ({e})", file=sys.stderr)
                     comm = None
-                if comm is not None and check_comm_gather(comm, dev):
+                # every rank takes the same branch: the check is a collective
+                up = torch.tensor([0 if comm is None else 1], dtype=torch.int64)
+                dist.all_reduce(up, op=dist.ReduceOp.MIN)
+                if int(up.item()) == 1 and check_comm_gather(comm, dev):
                     comm_used = "capi-rccl"
                 else:
                     if comm is not None:

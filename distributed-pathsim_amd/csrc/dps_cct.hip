@@ -703,7 +703,9 @@ extern "C" {
 
 // 64 counters; the profiling build adds four words per wave of the lean
 // kernel (start, end, start of its last row, that row) for tools/wave_times.py
-size_t dps_cct_topk_workspace_size(void) { return kProfile ? 512 + 32 * 16384 : 512; }
+// (profiling build: + per-wave realtime stamps, 32 B x 16384 waves, and per-row
+// time and passes, 8 B x 2^21 dequeue slots)
+size_t dps_cct_topk_workspace_size(void) { return kProfile ? 512 + 32 * 16384 + 8 * (1 << 21) : 512; }
 
 size_t dps_heavy_first_workspace_size(int64_t n_rows) {
   const size_t m = static_cast<size_t>(n_rows > 0 ? n_rows : 1);

@@ -1364,9 +1364,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
     if (r >= kcold(n_rows)) break;
     const int32_t* row_order = kcold(row_order);
     const int x = row_order ? row_order[r] : static_cast<int>(kcold(row_begin) + r);   // < 2^31
+    uint32_t np_row = 0;                // profiling build: passes before this row
     if (prof) {
       rt_last = __builtin_amdgcn_s_memrealtime();
       x_last = r;
+      np_row = n_pass;
     }
     const bool is_piece = r < kcold(n_pieces);
     int t_beg = is_piece ? kcold(piece_t0)[r] : 0;
@@ -1758,6 +1760,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(
       os[s2] = 0.0;
     }
     if (SY && p.sym == 2) sym_publish<KPL>(p, x_lab, strong, top, lane);
+    // profiling build: per dequeue slot r, (realtime ticks << 32) | passes of
+    // the row, at counter[64 + 4 * 16384 + r] (tools/row_times.py)
+    if (prof && lane == 0 && r < (1 << 21))
+      p.counter[64 + 4 * 16384 + r] = ((__builtin_amdgcn_s_memrealtime() - rt_last) << 32) |
+                                      static_cast<unsigned long long>(n_pass - np_row);
   }
   if (lane == 0 && (n_pass | n_chunk)) {
     unsigned long long* ctr = kcold(counter);

@@ -12,36 +12,53 @@ namespace {
 
 constexpr int kSelT = 1024;
 
-__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* red) {
-  v = wave_sum(v);
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  __syncthreads();                       // red is reused across calls
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  uint32_t t = 0;
-#pragma unroll
-  for (int i = 0; i < kSelT / kWave; ++i) t += red[i];
-  return t;
-}
-
 // One workgroup: the smallest threshold thr >= 1 with |{v : n_v >= thr}| <=
-// n_hv (binary search over the 32-bit range), then slots in venue order for
-// the venues at or above it.
+// n_hv, i.e. one above the (n_hv + 1)-th largest n_v (1 when there are at most
+// n_hv venues), found by an MSB-first radix select (four 8-bit digit passes,
+// an LDS histogram each; round 6 -- a 32-step binary search over the value
+// range took ~0.1 ms of config3's build); then slots in venue order for the
+// venues at or above it.
 __global__ __launch_bounds__(kSelT) void k_hv_select(const uint32_t* __restrict__ n_v, int64_t n_mids,
                                                      int n_hv, int32_t* __restrict__ hv_slot) {
-  __shared__ uint32_t red[kSelT / kWave];
+  __shared__ uint32_t hist[256];
   __shared__ uint32_t pre[kSelT];
+  __shared__ uint32_t sel[2];            // digit, count above it
   const int tid = threadIdx.x;
-  uint64_t lo = 1, hi = 1ull << 32;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    uint32_t cnt = 0;
-    for (int64_t i = tid; i < n_mids; i += kSelT) cnt += static_cast<uint64_t>(n_v[i]) >= mid;
-    cnt = block_sum_u32(cnt, red);
-    if (cnt <= static_cast<uint32_t>(n_hv)) hi = mid;
-    else lo = mid + 1;
+  uint64_t thr = 1;
+  if (n_mids > n_hv) {
+    uint32_t prefix = 0, mask = 0, want = static_cast<uint32_t>(n_hv) + 1u;   // rank, descending
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      if (tid < 256) hist[tid] = 0;
+      __syncthreads();
+      for (int64_t i = tid; i < n_mids; i += kSelT) {
+        const uint32_t v = n_v[i];
+        if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid < kWave) {
+        // lane l holds bins 4l..4l+3; above = the count in the bins past them
+        uint32_t h[4], own = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { h[j] = hist[4 * tid + j]; own += h[j]; }
+        const uint32_t incl = wave_inclusive_sum(own);
+        const uint32_t total = __shfl(incl, kWave - 1, kWave);
+        uint32_t above = total - incl;
+        if (above < want && want <= above + own) {
+#pragma unroll
+          for (int j = 3; j >= 0; --j) {
+            if (above < want && want <= above + h[j]) { sel[0] = 4u * tid + j; sel[1] = above; }
+            above += h[j];
+          }
+        }
+      }
+      __syncthreads();
+      prefix |= sel[0] << shift;
+      mask |= 255u << shift;
+      want -= sel[1];
+      __syncthreads();                   // sel / hist reused by the next pass
+    }
+    thr = static_cast<uint64_t>(prefix) + 1u;
   }
-  const uint64_t thr = lo;
   // contiguous venue ranges per thread, exclusive scan of their heavy counts
   const int64_t per = (n_mids + kSelT - 1) / kSelT;
   const int64_t b = tid * per, e = b + per < n_mids ? b + per : n_mids;

@@ -78,6 +78,46 @@ __global__ __launch_bounds__(kBlock) void k_block_scan(const T* __restrict__ in,
   if (n > 0 && base <= n - 1 && n - 1 < base + kItems) out[n] = run;
 }
 
+// The same scan whose block offset is the sum of the block reductions before
+// it, read here (round 6: for up to kDirectBlocks blocks this replaces the
+// separate single-block scan of the partial sums -- one launch fewer per scan,
+// ~4.5 us each, nine scans per config3 build).
+constexpr int64_t kDirectBlocks = 1024;
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_block_scan_direct(const T* __restrict__ in, int64_t n,
+                                                              const int64_t* __restrict__ partial,
+                                                              int64_t* __restrict__ out) {
+  __shared__ int64_t lds[kBlock / kWave];
+  __shared__ int64_t off_s;
+  int64_t o = 0;
+  for (int64_t i = threadIdx.x; i < blockIdx.x; i += kBlock) o += partial[i];
+  o = wave_sum(o);
+  if (lane_id() == 0) lds[threadIdx.x / kWave] = o;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int w = 0; w < kBlock / kWave; ++w) t += lds[w];
+    off_s = t;
+  }
+  __syncthreads();             // (lds is reused by block_exclusive)
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kTile + threadIdx.x * kItems;
+  int64_t v[kItems];
+  int64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kItems; ++i) {
+    v[i] = load_or0(in, base + i, n);
+    s += v[i];
+  }
+  int64_t total;
+  int64_t run = block_exclusive(s, lds, &total) + off_s;
+#pragma unroll
+  for (int i = 0; i < kItems; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+  if (n > 0 && base <= n - 1 && n - 1 < base + kItems) out[n] = run;
+}
+
 __global__ void k_zero_total(int64_t* out) { out[0] = 0; }
 
 }  // namespace
@@ -113,6 +153,10 @@ hipError_t scan_exclusive(const T* in, int64_t* out, int64_t n, void* ws, size_t
   k_block_reduce<T><<<static_cast<unsigned>(nb), kBlock, 0, stream>>>(in, n, partial);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (nb <= kDirectBlocks) {
+    k_block_scan_direct<T><<<static_cast<unsigned>(nb), kBlock, 0, stream>>>(in, n, partial, out);
+    return hipGetLastError();
+  }
   e = scan_exclusive<int64_t>(partial, pscan, nb, c.base + c.off, c.cap - c.off, stream);
   if (e != hipSuccess) return e;
   k_block_scan<T><<<static_cast<unsigned>(nb), kBlock, 0, stream>>>(in, n, pscan, out);

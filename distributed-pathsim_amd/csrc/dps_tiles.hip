@@ -716,7 +716,8 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_dual(
     TileDim tdB, int64_t TB, int labels_per_block, int PA, int PB, int S, int n_ranges,
     const uint32_t* __restrict__ part_n, uint32_t* __restrict__ cntpA, uint32_t* __restrict__ mxpA,
     uint32_t* __restrict__ cntpB, uint32_t* __restrict__ mxpB,
-    unsigned long long* __restrict__ gmin, int32_t* __restrict__ status) {
+    unsigned long long* __restrict__ gmin, int32_t* __restrict__ status,
+    const int32_t* __restrict__ hv_slot, int n_hv, uint16_t* __restrict__ hv_c) {
   __shared__ uint32_t cntA_s[kBlkMids];
   __shared__ uint32_t cntB_s[kBlkMids];
   __shared__ uint32_t mx_s[kBlkMids];
@@ -755,6 +756,10 @@ __global__ __launch_bounds__(kBlkThreads) void k_tile_count_dual(
     atomicAdd(&cntA_s[lv], n_pieces(fmtA, static_cast<uint32_t>(c), lab));
     atomicAdd(&cntB_s[lv], n_pieces(fmtB, static_cast<uint32_t>(c), lab));
     if (c > 1) atomicMax(&mx_s[lv], static_cast<uint32_t>(c));
+    if (hv_c) {   // the heavy-venue table (dps_heavy_table's layout), same walk
+      const int sl = hv_slot[v];
+      if (sl >= 0) hv_c[static_cast<int64_t>(lab) * n_hv + sl] = static_cast<uint16_t>(c < 0xFFFF ? c : 0xFFFF);
+    }
   });
   __syncthreads();
   if (threadIdx.x == 0 && ovf_s && status) *status = DPS_ERR_OVERFLOW;
@@ -1600,7 +1605,8 @@ int dps_ct_tiles_build_dual(const int64_t* c_ptr, const int32_t* c_col, const in
                             uint32_t* tile_ent, int64_t tile_ent_words, uint32_t* tile_maxc,
                             int64_t* tile_gmin, uint32_t* half_off, uint32_t* half_ent,
                             int64_t half_ent_words, uint32_t* half_maxc, int32_t* status_dev,
-                            int32_t* half_status, void* ws, size_t ws_bytes, void* stream) {
+                            int32_t* half_status, const int32_t* hv_slot, int32_t n_hv,
+                            uint16_t* hv_c, void* ws, size_t ws_bytes, void* stream) {
   const TileDim tdA = tile_dim(tile_w), tdB = tile_dim(tile_w / 2);
   DPS_REQUIRE(tdA.shift == 14 && tdB.shift == 13 && tdA.t15 == tdB.t15, DPS_ERR_UNSUPPORTED,
               "the dual build takes tile_w 16384 or 15360 (4-bit tiles), got %d", tile_w);
@@ -1608,22 +1614,29 @@ int dps_ct_tiles_build_dual(const int64_t* c_ptr, const int32_t* c_col, const in
   DPS_REQUIRE(n_targets < INT32_MAX, DPS_ERR_OVERFLOW, "n_targets exceeds int32");
   DPS_REQUIRE(!tile_gmin || g, DPS_ERR_INVALID, "tile_gmin needs g");
   DPS_REQUIRE(tile_off && tile_ent && half_off && half_ent, DPS_ERR_INVALID, "null tile arrays");
+  DPS_REQUIRE(!hv_c || (hv_slot && n_hv >= 1 && n_hv <= 64), DPS_ERR_INVALID,
+              "hv_c needs hv_slot and n_hv in [1, 64]");
   DPS_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 256 == 0, DPS_ERR_WORKSPACE,
               "workspace not 256-byte aligned");
   DPS_REQUIRE(ws_bytes >= dps_ct_tiles_workspace_size_dual(n_mids, n_targets, tile_w, nnz_cap),
               DPS_ERR_WORKSPACE, "tiles workspace too small");
   const int32_t hw = tile_w / 2;
+  // the heavy table from the count walk: zeroed with the counters (as words:
+  // even n_hv and a 4-byte aligned table), else by dps_heavy_table after
+  const bool hv_fused = hv_c && (n_hv & 1) == 0 && (reinterpret_cast<uintptr_t>(hv_c) & 3u) == 0;
   // many mids, or 16-bit entry offsets beyond the scatter's 32-bit cursors:
   // the two builds one after the other (they reuse the workspace)
   if (tile_global(n_mids) || 2 * tile_ent_words >= (int64_t(1) << 32) ||
       2 * half_ent_words >= (int64_t(1) << 32)) {
-    const int rc = dps_ct_tiles_build2(c_ptr, c_col, c_val, g, t_rank, n_targets, n_mids, tile_w,
-                                       nnz_cap, tile_off, tile_ent, tile_maxc, tile_gmin,
-                                       status_dev, ws, ws_bytes, stream);
+    int rc = dps_ct_tiles_build2(c_ptr, c_col, c_val, g, t_rank, n_targets, n_mids, tile_w,
+                                 nnz_cap, tile_off, tile_ent, tile_maxc, tile_gmin,
+                                 status_dev, ws, ws_bytes, stream);
     if (rc != DPS_OK) return rc;
-    return dps_ct_tiles_build2(c_ptr, c_col, c_val, nullptr, t_rank, n_targets, n_mids, hw,
-                               nnz_cap, half_off, half_ent, half_maxc, nullptr, half_status, ws,
-                               ws_bytes, stream);
+    rc = dps_ct_tiles_build2(c_ptr, c_col, c_val, nullptr, t_rank, n_targets, n_mids, hw,
+                             nnz_cap, half_off, half_ent, half_maxc, nullptr, half_status, ws,
+                             ws_bytes, stream);
+    if (rc != DPS_OK || !hv_c) return rc;
+    return dps_heavy_table(c_ptr, c_col, c_val, t_rank, n_targets, hv_slot, n_hv, hv_c, stream);
   }
   auto st = static_cast<hipStream_t>(stream);
   const int64_t TA = (n_targets + tile_w - 1) / tile_w, TB = (n_targets + hw - 1) / hw;
@@ -1665,6 +1678,8 @@ int dps_ct_tiles_build_dual(const int64_t* c_ptr, const int32_t* c_col, const in
     if (tile_gmin && TA > 0) fs.add(tile_gmin, 2 * TA, 0x7F7F7F7Fu);
     if (tile_maxc) fs.add(tile_maxc + nbA, 1, 0u);
     if (half_maxc) fs.add(half_maxc + nbB, 1, 0u);
+    if (hv_fused && n_targets > 0)
+      fs.add(reinterpret_cast<uint32_t*>(hv_c), n_targets * n_hv / 2, 0u);
     DPS_HIP_RET(fill_set(fs, st));
   }
   if (n_targets > 0 && nblk <= kPartLds) {
@@ -1687,8 +1702,13 @@ int dps_ct_tiles_build_dual(const int64_t* c_ptr, const int32_t* c_col, const in
     k_tile_count_dual<<<grid, kBlkThreads, 0, st>>>(
         c_ptr, c_col, c_val, perm_or_null, tile_gmin ? g : nullptr, n_targets, n_mids, tdA, TA, tdB,
         TB, lpb, PA, PB, S, n_ranges, part_n, cntpA, mxpA, cntpB, mxpB,
-        reinterpret_cast<unsigned long long*>(tile_gmin), status_dev);
+        reinterpret_cast<unsigned long long*>(tile_gmin), status_dev, hv_slot, n_hv,
+        hv_fused ? hv_c : nullptr);
     DPS_LAUNCHED();
+  }
+  if (hv_c && !hv_fused) {
+    const int rc = dps_heavy_table(c_ptr, c_col, c_val, t_rank, n_targets, hv_slot, n_hv, hv_c, stream);
+    if (rc != DPS_OK) return rc;
   }
   if (nbA > 0) {
     k_tile_parts_fix<<<grid_for(nbA, kBlock), kBlock, 0, st>>>(cntpA, mxpA, nbA, PA, 8u, cntA,

@@ -88,7 +88,8 @@ SIGNATURES = {
                                      _p, _sz, _p]),
     "dps_ct_tiles_workspace_size_dual": (_sz, [_i64, _i64, _i32, _i64]),
     "dps_ct_tiles_build_dual": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _i32, _i64, _p, _p, _i64,
-                                          _p, _p, _p, _p, _i64, _p, _p, _p, _p, _sz, _p]),
+                                          _p, _p, _p, _p, _i64, _p, _p, _p, _p, _i32, _p, _p, _sz,
+                                          _p]),
     "dps_cct_topk_workspace_size": (_sz, []),
     "dps_cct_topk": (C.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p,
                                _i64, _i64, _p, _i32, _p, _p, _p, _p, _sz, _p]),

@@ -43,15 +43,22 @@ class RcclComm:
                        else torch.device(device))
         nb = int(lib.dps_comm_id_bytes())
         buf = (C.c_uint8 * nb)()
+        err = ""
         if self.rank == 0:
-            _lib.call("dps_comm_get_id", C.addressof(buf))
+            try:
+                _lib.call("dps_comm_get_id", C.addressof(buf))
+            except RuntimeError as e:   # broadcast the failure too: no rank waits forever
+                err = str(e)
         cpu = dist.get_backend(group) != "nccl"
-        t = torch.tensor(bytearray(buf), dtype=torch.uint8,
+        t = torch.tensor(bytearray(buf) + bytes([0 if err else 1]), dtype=torch.uint8,
                          device="cpu" if cpu else self.device)
         # src is a GLOBAL rank: the group's rank 0 (a subgroup need not hold rank 0)
         src = 0 if group is None else dist.get_global_rank(group, 0)
         dist.broadcast(t, src=src, group=group)
-        buf = (C.c_uint8 * nb)(*t.cpu().tolist())
+        b = t.cpu().tolist()
+        if b[nb] != 1:
+            raise RuntimeError(f"dps_comm_get_id failed on rank 0 {err}".rstrip())
+        buf = (C.c_uint8 * nb)(*b[:nb])
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             _lib.call("dps_comm_init", C.addressof(h), self.world, self.rank, C.addressof(buf))

@@ -144,6 +144,7 @@ class PathSimEngine:
         self.checked = False
         self._dev = {}
         self._piece_cache = {}
+        self._last_dq = None       # the last top-k launch's dequeue list
 
     # ------------------------------------------------------------------ utils
     @property
@@ -320,6 +321,7 @@ class PathSimEngine:
                 tile_off, tile_ent, tile_maxc, tile_gmin, status = self._split_tiles(
                     split, sub, self.tile_w, g_t, True, ent_cap)
             elif dual:
+                hv_slot, hv_c, nh = self._heavy_venues(n_v, NA, NV, st)
                 HW = self.tile_w // 2
                 T8 = max(1, math.ceil(NA / HW)) if NA else 1
                 h_cap = _lib.size("dps_ct_tiles_ent_capacity", bnd.expand, bnd.sum_c, NV, NA, HW)
@@ -338,7 +340,8 @@ class PathSimEngine:
                           _ptr(den), _ptr(t_rank), NA, NV, self.tile_w, bnd.expand, _ptr(tile_off),
                           _ptr(tile_ent), tile_ent.numel(), _ptr(tile_maxc), _ptr(tile_gmin),
                           _ptr(h_off), _ptr(h_ent), h_ent.numel(), _ptr(h_maxc), _ptr(status),
-                          _ptr(h_status), _ptr(tws), tws.numel(), st)
+                          _ptr(h_status), _ptr(hv_slot), nh, _ptr(hv_c), _ptr(tws), tws.numel(),
+                          st)
                 del tws
                 t_sum = None            # (the optimistic passes' sums, as below)
                 if self.opt_passes and self.tile_w not in T15_TILE_W:
@@ -393,17 +396,12 @@ class PathSimEngine:
                 half = (h_off, h_ent, h_maxc, h_status, t_sum)
                 mark("half_tiles")
             del sub
-            hv_slot = hv_c = None
-            if self.venue_skip and self.denominator == "rowsum" and NA and NV:
-                # venue skipping: the heavy venues (most author entries) and the
-                # dense table of C over them, by target label
-                nh = min(self.n_heavy, 64)
-                hv_slot = self._empty(NV, torch.int32)
-                hv_c = self._empty(NA * nh, torch.int16)
-                _lib.call("dps_heavy_venues", _ptr(n_v), NV, nh, _ptr(hv_slot), st)
-                _lib.call("dps_heavy_table", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(t_rank), NA,
-                          _ptr(hv_slot), nh, _ptr(hv_c), st)
-                mark("heavy")
+            if not dual:
+                hv_slot, hv_c, nh = self._heavy_venues(n_v, NA, NV, st)
+                if hv_c is not None:
+                    _lib.call("dps_heavy_table", _ptr(c_ptr), _ptr(c_col), _ptr(c_val), _ptr(t_rank),
+                              NA, _ptr(hv_slot), nh, _ptr(hv_c), st)
+                    mark("heavy")
         d.pop("row_work", None)
         d.update(row_terms=terms, ap_ptr=ap_ptr, ap_col=ap_col, px_ptr=px_ptr, px_col=px_col, c_ptr=c_ptr,
                  c_col=c_col, c_val=c_val, c_nnz=c_nnz, s=s, g=g, diag=diag, den=den, g_t=g_t,
@@ -589,9 +587,22 @@ class PathSimEngine:
                 d["row_work"] = terms + (terms.sum() // max(NA, 1)) // 2
         return self._dev["row_work"]
 
+    def _heavy_venues(self, n_v, NA, NV, st):
+        """Venue skipping: the heavy venues (most author entries) -> hv_slot,
+        and the (unfilled) dense table of C over them by target label; (None,
+        None, 0) when venue skipping is off."""
+        if not (self.venue_skip and self.denominator == "rowsum" and NA and NV):
+            return None, None, 0
+        nh = min(self.n_heavy, 64)
+        hv_slot = self._empty(NV, torch.int32)
+        hv_c = self._empty(NA * nh, torch.int16)
+        _lib.call("dps_heavy_venues", _ptr(n_v), NV, nh, _ptr(hv_slot), st)
+        return hv_slot, hv_c, nh
+
     # ------------------------------------------------------------------ top-k
     def topk(self, k: int, row_begin: int = 0, row_end: int | None = None, out=None,
-             heavy_first: bool = True, split_rows: int | None = None, pieces: int | None = None):
+             heavy_first: bool = True, split_rows: int | None = None, pieces: int | None = None,
+             row_work: torch.Tensor | None = None):
         """★ all-pairs top-k for author rows [row_begin, row_end) (device tensors).
 
         ``heavy_first`` dequeues the rows in descending ``row_work`` order (LPT),
@@ -601,7 +612,8 @@ class PathSimEngine:
         the same launch, by separate waves) and their piece lists merged after
         (dps_topk_merge): a single heavy row then no longer bounds the launch --
         which matters most for the small per-rank shards of an N-GPU run.  The
-        results are identical either way."""
+        results are identical either way.  ``row_work`` (int64, one per row of
+        the range) replaces the build's ``row_terms`` as the dequeue key."""
         if not self.built:
             raise RuntimeError("call build() first")
         NA = self.typed.n_authors
@@ -636,9 +648,16 @@ class PathSimEngine:
                 # radix pass), the M heaviest as M*P pieces in front
                 dq = torch.empty(R + M * (P - 1), dtype=torch.int32, device=self.device)
                 hws = self._ws(_lib.size("dps_heavy_first_workspace_size", R))
-                _lib.call("dps_heavy_first", _ptr(d["row_terms"][row_begin:row_end]), R,
+                wk = d["row_terms"][row_begin:row_end]
+                if row_work is not None:
+                    if (row_work.numel() != R or row_work.dtype != wk.dtype
+                            or row_work.device != wk.device):
+                        raise ValueError("row_work: one int64 per row of the range, on the device")
+                    wk = row_work.contiguous()
+                _lib.call("dps_heavy_first", _ptr(wk), R,
                           int(row_begin), M, P if M else 1, _ptr(dq), _ptr(hws), hws.numel(),
                           self.stream)
+            self._last_dq = dq      # (tools/row_times.py: dequeue slot -> row)
             if M == 0:
                 _lib.call("dps_cct_topk", *common, int(row_begin), int(row_end), _ptr(dq),
                           int(k), _ptr(idx), _ptr(cnt), _ptr(sc), _ptr(d["topk_ws"]),

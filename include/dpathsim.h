@@ -325,9 +325,12 @@ int dps_ct_tiles_build2(const int64_t* c_ptr, const int32_t* c_col, const int32_
  * bucket), which it makes itself with many mids (more than 8 * 8192) or when
  * the entry buffers' sizes (tile_ent_words / half_ent_words, uint32 words) reach
  * 2^31.  Overflow (max C > 65535) goes to *status_dev; *half_status is zeroed
- * (and set only by the two-call path).  ws: dps_ct_tiles_workspace_size_dual
- * (0 for other widths).  Replaces nothing in the reference (layout only); A5's
- * operand build, DPathSim_APVPA.py:90-109. */
+ * (and set only by the two-call path).  hv_c (optional, with hv_slot / n_hv
+ * from dps_heavy_venues): the venue-skipping table of dps_heavy_table, written
+ * by the same walk (zeroed with the build's counters) when n_hv is even and
+ * hv_c 4-byte aligned, else by a dps_heavy_table call.  ws:
+ * dps_ct_tiles_workspace_size_dual (0 for other widths).  Replaces nothing in
+ * the reference (layout only); A5's operand build, DPathSim_APVPA.py:90-109. */
 size_t dps_ct_tiles_workspace_size_dual(int64_t n_mids, int64_t n_targets, int32_t tile_w,
                                         int64_t nnz_cap);
 int dps_ct_tiles_build_dual(const int64_t* c_ptr, const int32_t* c_col, const int32_t* c_val,
@@ -336,7 +339,8 @@ int dps_ct_tiles_build_dual(const int64_t* c_ptr, const int32_t* c_col, const in
                             uint32_t* tile_ent, int64_t tile_ent_words, uint32_t* tile_maxc,
                             int64_t* tile_gmin, uint32_t* half_off, uint32_t* half_ent,
                             int64_t half_ent_words, uint32_t* half_maxc, int32_t* status_dev,
-                            int32_t* half_status, void* ws, size_t ws_bytes, void* stream);
+                            int32_t* half_status, const int32_t* hv_slot, int32_t n_hv,
+                            uint16_t* hv_c, void* ws, size_t ws_bytes, void* stream);
 /* Per-bucket count sums of built tiles: tile_sum[b] = sum over the bucket's
  * entries of their values (2^e of a 16-bit piece, padding codes excluded; C of
  * a 32-bit entry) = sum_{y of tile t} C[y,v] for bucket b = v*T + t, b <

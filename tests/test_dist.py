@@ -416,10 +416,13 @@ def _rccl_capi_worker(rank, world, port, k, result_path):
     comm = None
     try:
         import pathsim_oracle as po
-        from dpathsim.dist import RcclComm, pack_counts
+        from dpathsim.dist import RcclComm, check_comm_gather, pack_counts
         from dpathsim.engine import build_engine
         from dpathsim.synth import synth_dblp
         comm = RcclComm()
+        # bench.py's pre-loop known-pattern check through the real communicator
+        if not check_comm_gather(comm, "cuda:0"):
+            raise AssertionError("check_comm_gather failed through RcclComm")
         t = synth_dblp(4000, 12000, 200, seed=8).typed()
         eng = build_engine(t, device="cuda:0")
         na = t.n_authors

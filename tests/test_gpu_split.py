@@ -176,3 +176,35 @@ def test_split_plan_is_per_graph():
     got = [a.cpu().numpy() for a in e2.topk(10)]
     assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
     assert np.array_equal(got[2].view(np.int64), want[2].view(np.int64))
+
+
+@pytest.mark.parametrize("tile_w", [16384, 15360])
+def test_dual_build_equals_two_builds(tile_w):
+    """dps_ct_tiles_build_dual (round 6: both tile sets and the heavy-venue
+    table from one walk of C) against two dps_ct_tiles_build2 calls and
+    dps_heavy_table: offsets, maxima, tile minima and the heavy table bit for
+    bit, every bucket's entries as a multiset."""
+    from dpathsim.engine import PathSimEngine
+    from dpathsim.synth import synth_config
+    t = synth_config("config3", scale=0.05).typed()
+    engs = []
+    for dual in (True, False):
+        e = PathSimEngine(t, tile_w=tile_w)
+        e.dual_build = dual
+        e.upload().build()
+        engs.append(e)
+    a, b = engs
+    NA, NV = t.n_authors, t.n_mids
+    for w, o_n, e_n, m_n in ((tile_w, "tile_off", "tile_ent", "tile_maxc"),
+                             (tile_w // 2, "half_off", "half_ent", "half_maxc")):
+        T = -(-NA // w)
+        oa = a.tensor(o_n)[: NV * T + 1].cpu().numpy().view(np.uint32).astype(np.int64)
+        ob = b.tensor(o_n)[: NV * T + 1].cpu().numpy().view(np.uint32).astype(np.int64)
+        assert np.array_equal(oa, ob), f"offsets differ at {w}"
+        assert torch.equal(a.tensor(m_n)[: NV * T], b.tensor(m_n)[: NV * T]), w
+        assert _bucket_multisets_equal(oa, a.tensor(e_n).cpu().numpy(), ob,
+                                       b.tensor(e_n).cpu().numpy(), w), f"entries differ at {w}"
+    T = -(-NA // tile_w)
+    assert torch.equal(a.tensor("tile_gmin")[:T], b.tensor("tile_gmin")[:T])
+    assert a.tensor("hv_c") is not None and torch.equal(a.tensor("hv_c"), b.tensor("hv_c"))
+    assert torch.equal(a.tensor("hv_slot"), b.tensor("hv_slot"))

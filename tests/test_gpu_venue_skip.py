@@ -92,3 +92,44 @@ def test_venue_skip_diag_denominator_is_off():
     t = synth_dblp(5_000, 15_000, 200, seed=2).typed()
     eng = build_engine(t, tile_w=8192, denominator="diag")
     assert (eng._ext is None or not eng._ext.s) and eng.tensor("hv_c") is None
+
+
+@pytest.mark.parametrize("n_hv,perm,n", [(32, True, 50_000), (32, False, 3), (31, True, 20_000),
+                                         (64, True, 20_000), (2, True, 1000)])
+def test_heavy_table_against_host(n_hv, perm, n):
+    """dps_heavy_table (whole rows for n_hv = 32 / 64 since round 6, the scattered
+    2-byte form otherwise) against the dense table built on the host: rows
+    with up to 300 venues, counts above 65535 saturated, labels permuted."""
+    import torch
+    from dpathsim import _lib
+    rng = np.random.default_rng(n_hv * 7 + n)
+    nv = 4000
+    deg = np.minimum(rng.geometric(0.15, n), 300)
+    deg[: min(3, n)] = [300, 0, 1][: min(3, n)]
+    ptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    col = np.concatenate([np.sort(rng.choice(nv, d, replace=False)) for d in deg]).astype(np.int32)
+    val = rng.integers(1, 200, len(col)).astype(np.int32)
+    val[:5] = [70000, 65535, 65534, 1, 2**31 - 1][: len(val[:5])]
+    n_v = np.bincount(col, minlength=nv).astype(np.uint32)
+    ranks = rng.permutation(n).astype(np.int32) if perm else None
+    dev = "cuda"
+    tt = lambda a: torch.from_numpy(a).to(dev)   # noqa: E731
+    # (device copies held in names until the kernels have run: a temporary's
+    # memory goes back to the caching allocator as soon as data_ptr() returns)
+    nv_d, ptr_d, col_d, val_d = tt(n_v.view(np.int32)), tt(ptr), tt(col), tt(val)
+    rk = tt(ranks) if perm else None
+    slot = torch.empty(nv, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    _lib.call("dps_heavy_venues", nv_d.data_ptr(), nv, n_hv, slot.data_ptr(), st)
+    hv = torch.full((n * n_hv,), 0x5A5A, dtype=torch.int16, device=dev)   # garbage: rows are written whole
+    _lib.call("dps_heavy_table", ptr_d.data_ptr(), col_d.data_ptr(), val_d.data_ptr(),
+              rk.data_ptr() if perm else None, n, slot.data_ptr(), n_hv, hv.data_ptr(), st)
+    torch.cuda.synchronize()
+    got = hv.cpu().numpy().view(np.uint16).reshape(n, n_hv)
+    sl = slot.cpu().numpy()
+    want = np.zeros((n, n_hv), np.uint16)
+    row = np.repeat(np.arange(n), deg)
+    lab = ranks[row] if perm else row
+    h = sl[col] >= 0
+    want[lab[h], sl[col][h]] = np.minimum(val[h], 0xFFFF).astype(np.uint16)
+    assert np.array_equal(got, want)

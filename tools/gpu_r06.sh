@@ -54,4 +54,23 @@ if [ -n "${AB:-}" ]; then
     done
   done
 fi
+if [ -n "${ROWS:-}" ]; then
+  DPATHSIM_LIB=$LIBDIR/libdpathsim_prof.so ROW_OUT=$O/row_times.npz timeout -k 10 300 \
+    python3 -u tools/row_times.py > $O/row_times_prof.txt 2>&1 || { echo "row prof failed"; tail -20 $O/row_times_prof.txt; exit 1; }
+  grep -v amdgpu.ids $O/row_times_prof.txt
+  ROW_PHASE=time ROW_OUT=$O/row_times.npz timeout -k 10 300 \
+    python3 -u tools/row_times.py > $O/row_times_ab.txt 2>&1 || { echo "row ab failed"; tail -20 $O/row_times_ab.txt; exit 1; }
+  grep -v amdgpu.ids $O/row_times_ab.txt
+fi
+if [ -n "${REHEARSE:-}" ]; then
+  # bench.py --gpus 2 over gloo on this one GPU (the driver's N > 1 runs use
+  # RCCL, one GPU per rank) and the C-ABI RCCL gather + known-pattern check
+  timeout -k 10 300 python -u -m pytest tests/test_dist.py -m gpu -x -v --timeout 240 \
+    --timeout-method thread > $O/pytest_dist.log 2>&1 || { echo "dist tests failed"; tail -30 $O/pytest_dist.log; exit 1; }
+  tail -2 $O/pytest_dist.log
+  DPATHSIM_BENCH_DEVICE=0 DPATHSIM_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run \
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 \
+    --steps 2 --warmup 1 > $O/bench_rehearse2.log 2>&1 || { echo "rehearsal failed"; tail -30 $O/bench_rehearse2.log; exit 1; }
+  grep '"metric"' $O/bench_rehearse2.log | cut -c1-400
+fi
 echo "session done"
