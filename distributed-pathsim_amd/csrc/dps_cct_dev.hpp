@@ -228,10 +228,16 @@ struct TopK {
           (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo)));
       uy[r] = __builtin_amdgcn_update_dpp(0, y[r], 0x138, 0xF, 0xF, false);
       um[r] = __builtin_amdgcn_update_dpp(0, m[r], 0x138, 0xF, 0xF, false);
-      if (r > 0 && lane == 0) {
-        us[r] = readlane(s[r - 1], kWave - 1);
-        uy[r] = readlane(y[r - 1], kWave - 1);
-        um[r] = readlane(m[r - 1], kWave - 1);
+      if (r > 0) {
+        // lane 0 <- lane 63 of the register below.  The readlanes run with the
+        // whole wave active: under `lane == 0` an -O1 build (registers spilled
+        // to scratch, the loop not unrolled) reloaded s[r - 1] for lane 0 only
+        // and read lane 63's stale copy (round 6, k > 64 in the debug build)
+        const double ps = readlane(s[r - 1], kWave - 1);
+        const int py = readlane(y[r - 1], kWave - 1), pm = readlane(m[r - 1], kWave - 1);
+        us[r] = lane == 0 ? ps : us[r];
+        uy[r] = lane == 0 ? py : uy[r];
+        um[r] = lane == 0 ? pm : um[r];
       }
     }
 #pragma unroll
