@@ -525,3 +525,38 @@ def test_check_comm_gather_verdict_on_every_rank(tmp_path, world):
     assert out.read_text() == "True,False,False"
     for r in range(1, world):
         assert (tmp_path / f"result.txt.{r}").read_text() == "True,False,False"
+
+
+def _comm_id_fail_worker(rank, world, port, result_path):
+    """RcclComm when rank 0 cannot create the RCCL unique id: the failure is
+    broadcast with the id's bytes, so every rank raises instead of waiting."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dpathsim import _lib
+        from dpathsim.dist import RcclComm
+        real = _lib.call
+
+        def call(name, *a):
+            if name == "dps_comm_get_id":
+                raise _lib.DPSError(name, _lib.DPS_ERR_HIP, "simulated ncclGetUniqueId failure")
+            if name == "dps_comm_init":
+                raise AssertionError("dps_comm_init reached after a failed unique id")
+            return real(name, *a)
+        _lib.call = call
+        try:
+            RcclComm(device="cpu")
+            msg = "no error"
+        except RuntimeError as e:
+            msg = "raised" if "dps_comm_get_id failed on rank 0" in str(e) else f"other: {e}"
+        with open(f"{result_path}.{rank}", "w") as f:
+            f.write(msg)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_comm_id_failure_reaches_every_rank(tmp_path):
+    out = tmp_path / "result.txt"
+    mp.start_processes(_comm_id_fail_worker, args=(2, _free_port(), str(out)), nprocs=2,
+                       join=True, start_method="spawn")
+    assert [open(f"{out}.{r}").read() for r in range(2)] == ["raised", "raised"]
