@@ -172,6 +172,9 @@ class PathSimEngine:
                 node_type=to(t.node_type if g.n_nodes else np.zeros(1, np.uint8)),
                 node_rowid=to(t.node_rowid if g.n_nodes else np.zeros(1, np.int32)),
                 node_colid=to(t.node_colid if g.n_nodes else np.zeros(1, np.int32)),
+                # the SpGEMM status of the gather and sort paths, which never
+                # write it: zeroed once here, so a build launches no fill for it
+                sp_zero=to(np.zeros(1, np.int32)),
             )
         if self.bounds is None:
             self.bounds = host_bounds(t)
@@ -248,11 +251,12 @@ class PathSimEngine:
             # the hash SpGEMM, kept as engine.spgemm = "hash").
             cap = bnd.sum_c
             c_ptr, c_nnz = self._empty(NR + 1, torch.int64), self._empty(2, torch.int64)
-            sp_status = self._empty(1, torch.int32)
+            # (the hash SpGEMM zeroes and sets its own status; the other two
+            # paths have none -- their status is the never-written zero word)
+            sp_status = d["sp_zero"] if (single or self.spgemm != "hash") else self._empty(1, torch.int32)
             c_col, c_val = self._empty(cap, torch.int32), self._empty(cap, torch.int32)
             if single:
                 sws = self._ws(_lib.size("dps_spgemm_single_workspace_size", NR, E, NP))
-                sp_status.zero_()
                 for numeric in (False, True):
                     _lib.call("dps_spgemm_single_map", _ptr(ap_ptr), _ptr(ap_col), NR, E, _ptr(vp),
                               None, None, NP, NV, _ptr(c_ptr), _ptr(c_col) if numeric else None,
@@ -262,7 +266,6 @@ class PathSimEngine:
             elif self.spgemm != "hash":
                 # expand + segmented sort/unique (sum_c bounds the expansion)
                 sws = self._ws(_lib.size("dps_spgemm_workspace_size", NR, bnd.sum_c))
-                sp_status.zero_()
                 for numeric in (False, True):
                     _lib.call("dps_spgemm_count", _ptr(ap_ptr), _ptr(ap_col), None, NR, _ptr(px_ptr),
                               _ptr(px_col), NP, _ptr(c_ptr), _ptr(c_col) if numeric else None,
